@@ -1,0 +1,164 @@
+/* lc_clip.h — C ABI of liblcclip.so, the MI355X (gfx950) kernels for the CLIP dual-encoder
+ * PEFT training step of qcNPU/LifeLong-CLIP (methods/adapter_clip.py:86-96).
+ *
+ * The reference has no FFI: its boundary is a torch.nn.Module (models/adapter_clip.py,
+ * models/clip/model.py) whose arithmetic is ATen. Each entry point below replaces the ATen call
+ * sites cited next to it; lifelong-clip_amd/lcclip binds them with ctypes behind the same
+ * nn.Module surface.
+ *
+ * Conventions (all entry points):
+ *  - plain device pointers + sizes; no allocation inside; re-entrant across streams/devices;
+ *  - `stream` is a hipStream_t (the caller's current stream);
+ *  - bf16 tensors are raw 16-bit bfloat16 bits; f32 tensors are IEEE float; ld* = row strides
+ *    in elements; all matrices are row-major;
+ *  - return 0 on success, LC_EINVAL (-1) on an argument/shape violation detected on the host
+ *    (nothing is launched), LC_ELAUNCH (-2) if the launch failed. The Python shim raises
+ *    RuntimeError on any nonzero return (the reference's own error behaviour is an exception
+ *    propagating to main(), nohup.out:30-43).
+ */
+#ifndef LC_CLIP_H
+#define LC_CLIP_H
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LC_OK 0
+#define LC_EINVAL (-1)
+#define LC_ELAUNCH (-2)
+
+/* GEMM epilogues for lc_gemm_nt */
+#define LC_EPI_BF16 0     /* out0 bf16 = alpha*acc + bias                                    */
+#define LC_EPI_F32 1      /* out0 f32  = alpha*acc + bias                                    */
+#define LC_EPI_RESID 2    /* out0 f32  = aux_f32 + alpha*acc + bias     (x + sublayer(x))    */
+#define LC_EPI_GELU 3     /* out0 bf16 = acc + bias; out1 bf16 = QuickGELU(acc + bias)        */
+#define LC_EPI_GELU_BWD 4 /* out0 bf16 = alpha*acc * QuickGELU'(aux_bf16)                    */
+#define LC_EPI_BF16_F32 5 /* out0 bf16 and out1 f32 of alpha*acc + bias                     */
+
+/* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0.
+ * Replaces: F.linear for QKV / out-proj (models/clip/lora.py:837, 1072; torch MHA for
+ * model.py:217,230), nn.Linear c_fc/c_proj + QuickGELU + residual adds (model.py:219-222,
+ * 234-235, 203-206), conv1 as a patch GEMM (model.py:709-713, 756), `@ proj` / `@
+ * text_projection` (model.py:785, 954), and the dX GEMMs of their autograd backward. */
+int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+               const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+               void* out1, long ldo1, const void* aux, long ldaux);
+
+/* C[N1,N2] += alpha * A[M,N1]^T . B[M,N2] (f32 C, atomically accumulated; split over M).
+ * Replaces: the autograd weight-gradient GEMMs of adapter down_proj / up_proj
+ * (models/clip/adapter.py:38-40, 59-62). */
+int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
+               long ldb, float alpha, float* C, long ldc);
+
+/* LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0), fp32 statistics, eps 1e-5.
+ * y is bf16 (y_f32 = 0) or f32 (y_f32 = 1); row_idx (optional) gathers input rows.
+ * mean/rstd (optional, f32[rows]) are saved for the backward.
+ * Replaces: LayerNorm.forward (model.py:194-200) for ln_1/ln_2/ln_pre/ln_post/ln_final. */
+int lc_layernorm_fwd(hipStream_t stream, int rows, int D, const float* x, long ldx,
+                     const int* row_idx, const float* gamma, const float* beta, void* y,
+                     int y_f32, long ldy, float* mean, float* rstd);
+
+/* dx[row_idx[r]] = dres[row_idx[r]] + LayerNorm_backward(dy[r]) (gamma/beta frozen), written
+ * as f32 (dx) and optionally bf16 (dx_bf16). dy is bf16 or f32 (dy_f32). dres may be NULL.
+ * Replaces: autograd of F.layer_norm (model.py:199). */
+int lc_layernorm_bwd(hipStream_t stream, int rows, int D, const void* dy, int dy_f32, long ldy,
+                     const float* x, long ldx, const float* mean, const float* rstd,
+                     const float* gamma, const float* dres, float* dx, void* dx_bf16, long ldo,
+                     const int* row_idx);
+
+/* im2col of NCHW f32 images into bf16 patches [n*g*g, 3*P*P] in conv1's (c, kh, kw) order.
+ * Replaces: the input side of conv1 (model.py:756-758). */
+int lc_patchify(hipStream_t stream, int n_img, int res, int patch, const float* img, void* out);
+
+/* x[n][0] = cls + pos[0]; x[n][1+p] = patch[n*np+p] + pos[1+p]   (model.py:759-764). */
+int lc_vit_assemble(hipStream_t stream, int n_img, int n_patch, int D, const float* patch,
+                    const float* cls, const float* pos, float* x);
+
+/* x[c][t] = emb[tokens[c][t]] + pos[t]   (model.py:943-946). */
+int lc_text_embed(hipStream_t stream, int C, int L, int D, const int64_t* tokens,
+                  const float* emb, const float* pos, float* x);
+
+/* row_idx[c] = c*L + argmax_t tokens[c][t]   (EOT pooling, model.py:953-954). */
+int lc_eot_rows(hipStream_t stream, int C, int L, const int64_t* tokens, int* row_idx);
+
+/* Multi-head attention core, d_head = 64, L <= 256 (bwd: L <= 224). qkv [n_seq*L, ldq] holds
+ * q|k|v at columns 0, H*64, 2*H*64; O [n_seq*L, ldo]; lse f32 [n_seq*H, L] (log2 domain).
+ * causal = 1 applies the text tower's upper-triangular -inf mask.
+ * Replaces: lora.py:950-1071 (q scaling, bmm, mask, softmax, dropout p=0, bmm) and the SDPA
+ * path of torch nn.MultiheadAttention (model.py:217,230), forward and backward. */
+int lc_attn_fwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq, void* O,
+                long ldo, float* lse, int causal);
+int lc_attn_bwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
+                const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
+                int causal);
+
+/* f32 -> bf16 cast of n elements (weight staging). */
+int lc_cast_bf16(hipStream_t stream, long n, const float* src, void* dst);
+
+/* out = bf16(W + scaling * B @ A) [N,K] and optionally outT = its transpose [K,N]; r = 0 casts W.
+ * Replaces: the LoRA residual of lora.py:838-839 (in-proj, A [r,D] shared by q/k/v, B [3D,r])
+ * and lora.py:1073-1074 / lora.Linear.forward :162-171 (out-proj), merged once per step. */
+int lc_merge_weight(hipStream_t stream, int N, int K, int r, const float* W, const float* A,
+                    const float* B, float scaling, void* out, void* outT);
+
+/* dB[N,r] += scaling * dY^T (X A^T);  dA[r,K] += scaling * (dY B)^T X   (r == 4).
+ * Replaces: autograd of the two F.linear LoRA products (lora.py:838-839, 1073-1074). */
+int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
+                 const void* X, long ldx, const float* A, const float* B, float scaling,
+                 float* dA, float* dB);
+
+/* xout = resid + z + scale*(drop(relu(z Wd^T + bd)) Wu^T + bu); h (bf16 [M,64]) is saved.
+ * keep = 1 - dropout p; seed selects the counter-based dropout mask.
+ * Replaces: Adapter.forward (adapter.py:53-72) + the block residual (model.py:440-441). */
+int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
+                   const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                   unsigned long long seed, const float* resid, float* xout, long ldx, void* h);
+
+/* Row-local adapter backward: dpre (bf16 [M,64]), dz = gout + dpre Wd (bf16), dbd += sum dpre,
+ * dbu += scale * sum gout. WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16).
+ * Replaces: autograd of adapter.py:59-72. */
+int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                   const void* WuT, const void* WdT, float scale, float keep, void* dpre,
+                   void* dz, long ldz, float* dbd, float* dbu);
+
+/* *flag |= any(!isfinite(g))  (GradScaler's inf check, _trainer.py:163, adapter_clip.py:94). */
+int lc_check_finite(hipStream_t stream, long n, const float* g, int* flag);
+
+/* torch.optim.AdamW step over a flat fp32 buffer; skipped when *skip != 0.
+ * Replaces: optimizer.step() (utils/train_utils.py:27-28, methods/adapter_clip.py:94). */
+int lc_adamw(hipStream_t stream, long n, float* p, const float* g, float* m, float* v, float lr,
+             float b1, float b2, float eps, float wd, int step, const int* skip);
+
+/* out[r] = f[r] / ||f[r]||, norms[r] = ||f[r]||   (model.py:966-969, adapter_clip.py:78). */
+int lc_l2norm_rows(hipStream_t stream, int R, int E, const float* f, long ldf, float* out,
+                   float* norms);
+
+/* Head forward+backward: logits = exp(*logit_scale) img_n txt_n^T, probs = softmax(logits),
+ * *loss += mean_b CE(probs_b, labels_b), dlogits = d loss / d logits. *loss must be zeroed.
+ * Replaces: model.py:972-973, models/adapter_clip.py:99, methods/adapter_clip.py:88-89. */
+int lc_clip_head(hipStream_t stream, int B, int C, int E, const float* img_n, const float* txt_n,
+                 const float* logit_scale, const int64_t* labels, float* probs, float* dlogits,
+                 float* loss);
+
+/* dF[r] = (dn - n (n.dn)) / norm[r], dn = exp(*logit_scale) sum_c dlog(r,c) other_n[c] + dn_ext[r];
+ * dlog(r,c) = dlogits[r*sr + c*sc]; dn_ext (grad arriving at the normalised features) may be
+ * NULL. Backward of the normalisation + logit GEMM (model.py:966-973). */
+int lc_head_feat_grad(hipStream_t stream, int R, int Co, int E, const float* dlogits, long sr,
+                      long sc, const float* other_n, const float* self_n, const float* norms,
+                      const float* logit_scale, const float* dn_ext, float* dF);
+
+/* logits = exp(*logit_scale) img_n txt_n^T [B,C]; probs = softmax(logits) when probs != NULL.
+ * Replaces: model.py:972-973 and models/adapter_clip.py:99 (module path). */
+int lc_head_logits(hipStream_t stream, int B, int C, int E, const float* img_n, const float* txt_n,
+                   const float* logit_scale, float* logits, float* probs);
+
+/* dlogits = probs * (dprobs - rowsum(probs * dprobs))   (softmax backward). */
+int lc_softmax_bwd_rows(hipStream_t stream, int B, int C, const float* probs, const float* dprobs,
+                        float* dlogits);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LC_CLIP_H */

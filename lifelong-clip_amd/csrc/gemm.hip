@@ -1,0 +1,337 @@
+// bf16 MFMA GEMMs for the CLIP PEFT step on gfx950.
+//
+//  lc_gemm_nt : C[M,N] = A[M,K] . B[N,K]^T (+bias) with a fused epilogue. Both operands are
+//               K-contiguous: activations [rows, features] and nn.Linear weights [out, in]
+//               (models/clip/model.py:219-222, lora.py:837/1072). The backward dX GEMMs use a
+//               transposed copy of each frozen weight kept resident in HBM, so every GEMM of
+//               the step (fwd and dX) runs through this one NT kernel.
+//  lc_gemm_tn : C[N1,N2] += alpha * A[M,N1]^T . B[M,N2], reduction over the M = batch*tokens
+//               rows, split over M across workgroups (PEFT weight gradients: adapter
+//               down/up, adapter.py:38-40).
+//
+// Tiling (NT): BM x BN x 64 block tile, 256 threads = 4 waves in a WM x WN grid, 16x16x32
+// bf16 MFMA. The MFMA is issued "swapped" (A-operand = weight rows, B-operand = activation
+// rows) so each lane's accumulator holds 4 consecutive output columns of one row: epilogue
+// stores are 8 B (bf16) / 16 B (f32) per lane. Tiles are staged global->LDS with
+// global_load_lds_dwordx4 into a lane-linear image; bank conflicts of the ds_read_b128 fragment
+// reads are removed by an XOR swizzle applied to the per-lane SOURCE chunk (chunk ^ ((row>>1)&7))
+// and to the read address. Two LDS buffers: the next K-tile's DMA overlaps this tile's MFMAs.
+// Grid: one workgroup per output tile, XCD-aware bijective remap so that the tiles an XCD
+// runs are contiguous in (m, n) order and share A row-panels in its L2.
+#include "lc_common.h"
+
+enum {
+  EPI_BF16 = 0,        // out0 bf16 = acc*alpha + bias
+  EPI_F32 = 1,         // out0 f32  = acc*alpha + bias
+  EPI_RESID = 2,       // out0 f32  = aux_f32 + acc*alpha + bias          (residual add)
+  EPI_GELU = 3,        // out0 bf16 = pre = acc+bias ; out1 bf16 = quick_gelu(pre)
+  EPI_GELU_BWD = 4,    // out0 bf16 = (acc*alpha) * quick_gelu'(aux_bf16)
+  EPI_BF16_F32 = 5,    // out0 bf16 and out1 f32 of acc*alpha + bias
+};
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+LC_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int ROWS>
+LC_DEV void stage_tile(const bf16_t* __restrict__ g, long ld, int row0, int rows_valid, int k0,
+                       char* lds, int tid) {
+  // ROWS x 64 bf16 tile = ROWS*128 bytes; one wave-instruction moves 8 rows (1 KiB).
+  constexpr int INSTR = ROWS / 8 / 4;  // per wave (4 waves)
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    int r = (wave * INSTR + i) * 8 + (lane >> 3);
+    int p = lane & 7;
+    int c = swz(r, p);  // global chunk that lands at LDS position p of row r
+    int gr = row0 + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;  // clamp: tail rows are computed, never stored
+    const bf16_t* src = g + (long)gr * ld + k0 + c * 8;
+    glds16(src, lds + (wave * INSTR + i) * 1024);
+  }
+}
+
+LC_DEV bf16x8 read_frag(const char* lds, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + swz(row, chunk) * 16);
+}
+
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(NT, 2)
+gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
+               const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
+               float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
+               long ldo1, const void* __restrict__ aux, long ldaux) {
+  constexpr int TM = BM / WM / 16;  // 16-row subtiles per wave (activation rows)
+  constexpr int TN = BN / WN / 16;  // 16-col subtiles per wave (output features)
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // XCD-aware bijective block remap.
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  auto stage = [&](int buf, int kt) {
+    char* s = smem + buf * STAGE_BYTES;
+    stage_tile<BM>(A, lda, m0, M, kt * BK, s, tid);
+    stage_tile<BN>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
+  };
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* sa = smem + cur * STAGE_BYTES;
+    const char* sb = sa + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = read_frag(sa, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = read_frag(sb, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds out[m][n..n+3], m = row of activation subtile, n = 4 consecutive cols.
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
+      if (EPI != EPI_GELU_BWD && bias != nullptr) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      }
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
+        uint2 pk = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
+        if constexpr (EPI == EPI_BF16_F32)
+          *reinterpret_cast<float4*>((float*)out1 + m * ldo1 + n) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (EPI == EPI_RESID) {
+        const float4 x = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n);
+        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) =
+            make_float4(x.x + v[0], x.y + v[1], x.z + v[2], x.w + v[3]);
+      } else if constexpr (EPI == EPI_GELU) {
+        uint2 pk = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
+        uint2 pg = {pack2bf(quick_gelu(v[0]), quick_gelu(v[1])),
+                    pack2bf(quick_gelu(v[2]), quick_gelu(v[3]))};
+        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) = pg;
+      } else if constexpr (EPI == EPI_GELU_BWD) {
+        const uint2 a = *reinterpret_cast<const uint2*>((const bf16_t*)aux + m * ldaux + n);
+        float g0 = quick_gelu_grad(bf2f(a.x & 0xffff)), g1 = quick_gelu_grad(bf2f(a.x >> 16));
+        float g2 = quick_gelu_grad(bf2f(a.y & 0xffff)), g3 = quick_gelu_grad(bf2f(a.y >> 16));
+        uint2 pk = {pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// TN split-K GEMM: C[N1,N2] += alpha * sum_m A[m][n1] * B[m][n2].
+// 64x64 output tile per workgroup, 4 waves (2x2, 32x32 each), K-step = 64 rows of M staged
+// row-major in LDS and read TRANSPOSED with ds_read_b64_tr_b16 (4 rows x 16 cols per 16-lane
+// group -> lane i gets column i), which is exactly the k-major fragment the MFMA needs.
+// Each workgroup reduces one chunk of M and adds its tile into C with f32 atomics.
+constexpr int TN_BM = 64;
+
+LC_DEV bf16x4 tr_read(const char* lds, int row, int col) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) bf16x4*)(lds + row * 128 + col * 2));
+}
+
+__global__ void __launch_bounds__(256)
+gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__ A, long lda,
+               const bf16_t* __restrict__ B, long ldb, float alpha, float* __restrict__ C,
+               long ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TN_BM * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wa = wave >> 1, wb = wave & 1;
+  const int tiles_n2 = N2 / 64;
+  const int t1 = blockIdx.x / tiles_n2, t2 = blockIdx.x % tiles_n2;
+  const int c1 = t1 * 64, c2 = t2 * 64;
+  const int mbeg = blockIdx.y * chunk_rows;
+  const int mend = min(M, mbeg + chunk_rows);
+  if (mbeg >= mend) return;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int mrow) {
+    char* s = smem + buf * (2 * TN_BM * 128);
+    // 64 rows x 128 B per operand = 8 wave-instructions; 2 per wave per operand.
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int r = (wave * 2 + i) * 8 + (lane >> 3);
+      int gr = min(mrow + r, mend - 1);
+      glds16(A + (long)gr * lda + c1 + (lane & 7) * 8, s + (wave * 2 + i) * 1024);
+      glds16(B + (long)gr * ldb + c2 + (lane & 7) * 8, s + TN_BM * 128 + (wave * 2 + i) * 1024);
+    }
+  };
+
+  const int nsteps = (mend - mbeg + TN_BM - 1) / TN_BM;
+  stage(0, mbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    const int mrow = mbeg + st * TN_BM;
+    if (st + 1 < nsteps) stage(cur ^ 1, mrow + TN_BM);
+    char* sa = smem + cur * (2 * TN_BM * 128);
+    char* sb = sa + TN_BM * 128;
+    const int valid = mend - mrow;
+    if (valid < TN_BM) {
+      // zero the rows past the end of M (they were loaded clamped)
+      for (int idx = tid; idx < (TN_BM - valid) * 16; idx += 256) {
+        int r = valid + idx / 16, c = (idx % 16) * 8;
+        if (c < 64) *reinterpret_cast<uint4*>(sa + r * 128 + c * 2) = uint4{0, 0, 0, 0};
+        else *reinterpret_cast<uint4*>(sb + r * 128 + (c - 64) * 2) = uint4{0, 0, 0, 0};
+      }
+      __syncthreads();
+    }
+    const int g = lane >> 4, t = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // rows (k) 32ks + 8g + {0..3}, {4..7}; cols block; lane 4q+p -> row q, cols 4p..4p+3
+        const int row = ks * 32 + g * 8 + (t >> 2);
+        const int cola = wa * 32 + i * 16 + (t & 3) * 4;
+        bf16x4 lo = tr_read(sa, row, cola), hi = tr_read(sa, row + 4, cola);
+        fa[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const int colb = wb * 32 + i * 16 + (t & 3) * 4;
+        bf16x4 lo2 = tr_read(sb, row, colb), hi2 = tr_read(sb, row + 4, colb);
+        fb[i] = bf16x8{lo2[0], lo2[1], lo2[2], lo2[3], hi2[0], hi2[1], hi2[2], hi2[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // acc[i][j]: lane holds D[n1 = 4g + r][n2 = t] of subtile (i, j)
+  const int g = lane >> 4, t = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n1 = c1 + wa * 32 + i * 16 + g * 4 + r;
+        const int n2 = c2 + wb * 32 + j * 16 + t;
+        atomicAdd(C + (long)n1 * ldc + n2, acc[i][j][r] * alpha);
+      }
+}
+
+template <int BM, int BN, int WM, int WN>
+int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
+              const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
+              void* o1, long l1, const void* aux, long la) {
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  dim3 grid(tiles), block(NT);
+#define LC_NT_CASE(E)                                                                        \
+  case E:                                                                                    \
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, E>), grid, block, 0, st, M, N, K, A,  \
+                       lda, B, ldb, bias, alpha, o0, l0, o1, l1, aux, la);                   \
+    break;
+  switch (epi) {
+    LC_NT_CASE(EPI_BF16)
+    LC_NT_CASE(EPI_F32)
+    LC_NT_CASE(EPI_RESID)
+    LC_NT_CASE(EPI_GELU)
+    LC_NT_CASE(EPI_GELU_BWD)
+    LC_NT_CASE(EPI_BF16_F32)
+    default:
+      return LC_EINVAL;
+  }
+#undef LC_NT_CASE
+  LC_LAUNCH_RET();
+}
+
+}  // namespace
+
+extern "C" {
+
+// See include/lc_clip.h for the contract.
+int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+               const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+               void* out1, long ldo1, const void* aux, long ldaux) {
+  LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
+  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
+  LC_CHECK_ARG(ldo0 % 4 == 0 && ldo0 >= N);
+  LC_CHECK_ARG(epi >= 0 && epi <= 5);
+  if (epi == EPI_GELU || epi == EPI_BF16_F32) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
+  if (epi == EPI_RESID || epi == EPI_GELU_BWD) LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 4 == 0);
+  auto a = static_cast<const bf16_t*>(A);
+  auto b = static_cast<const bf16_t*>(B);
+  if (N % 128 == 0)
+    return launch_nt<128, 128, 2, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                     ldo0, out1, ldo1, aux, ldaux);
+  return launch_nt<128, 64, 4, 1>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0,
+                                  out1, ldo1, aux, ldaux);
+}
+
+int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
+               long ldb, float alpha, float* C, long ldc) {
+  LC_CHECK_ARG(M > 0 && N1 % 64 == 0 && N2 % 64 == 0 && N1 > 0 && N2 > 0);
+  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= N1 && ldb >= N2 && ldc >= N2);
+  const int tiles = (N1 / 64) * (N2 / 64);
+  // Enough M-chunks to give ~4 workgroups per CU, each chunk a multiple of 64 rows.
+  int splits = (1024 + tiles - 1) / tiles;
+  int chunk = (M + splits - 1) / splits;
+  chunk = ((chunk + 63) / 64) * 64;
+  if (chunk < 256) chunk = 256;
+  splits = (M + chunk - 1) / chunk;
+  dim3 grid(tiles, splits), block(256);
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, block, 0, stream, M, N1, N2, chunk,
+                     static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(B), ldb, alpha,
+                     C, ldc);
+  LC_LAUNCH_RET();
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+// Image-text logit head, forward + backward in one pass over the (small) B x C logit block:
+//   models/clip/model.py:966-974  normalise, logits = exp(logit_scale) * I^ T^T
+//   models/adapter_clip.py:99      probs = softmax(logits)
+//   methods/adapter_clip.py:88-89  loss = CrossEntropyLoss(mean)(probs, y)   (CE on the
+//                                  probabilities — the reference's double softmax, Q5)
+// logit_scale is read from device memory (no host sync; it is frozen, Q12).
+#include "lc_common.h"
+
+namespace {
+
+__global__ void __launch_bounds__(64)
+l2norm_kernel(int R, int E, const float* __restrict__ f, long ldf, float* __restrict__ out,
+              float* __restrict__ norms) {
+  const int r = blockIdx.x, lane = threadIdx.x;
+  const float* row = f + (long)r * ldf;
+  float s = 0.f;
+  for (int k = lane; k < E; k += 64) s += row[k] * row[k];
+  const float nrm = sqrtf(wave_sum(s));
+  const float inv = 1.0f / nrm;
+  for (int k = lane; k < E; k += 64) out[(long)r * E + k] = row[k] * inv;
+  if (lane == 0) norms[r] = nrm;
+}
+
+// one workgroup (256 threads) per image row b
+__global__ void __launch_bounds__(256)
+head_rows_kernel(int B, int C, int E, const float* __restrict__ img_n,
+                 const float* __restrict__ txt_n, const float* __restrict__ logit_scale,
+                 const int64_t* __restrict__ labels, float* __restrict__ probs,
+                 float* __restrict__ dlogits, float* __restrict__ loss) {
+  extern __shared__ float sh[];  // [E] image row + [C] logits
+  float* irow = sh;
+  float* lg = sh + E;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float s = __expf(*logit_scale);
+  for (int k = tid; k < E; k += 256) irow[k] = img_n[(long)b * E + k];
+  __syncthreads();
+  for (int c = w; c < C; c += 4) {
+    float d = 0.f;
+    for (int k = lane; k < E; k += 64) d += irow[k] * txt_n[(long)c * E + k];
+    d = wave_sum(d);
+    if (lane == 0) lg[c] = s * d;
+  }
+  __syncthreads();
+  if (w != 0) return;
+  // softmax over logits -> p ; CE over p: loss_b = logsumexp(p) - p[y]
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, lg[c]);
+  m = wave_max(m);
+  float z = 0.f;
+  for (int c = lane; c < C; c += 64) z += __expf(lg[c] - m);
+  z = wave_sum(z);
+  // p in (0, 1]: logsumexp(p) needs no max shift
+  float z2 = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float p = __expf(lg[c] - m) / z;
+    lg[c] = p;
+    probs[(long)b * C + c] = p;
+    z2 += __expf(p);
+  }
+  z2 = wave_sum(z2);
+  const int y = (int)labels[b];
+  const float invB = 1.0f / B;
+  // dL/dp_c = (softmax(p)_c - [c == y]) / B ; dL/dlogit = p * (dp - sum p*dp)
+  float dot = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float p = lg[c];
+    const float dp = (__expf(p) / z2 - (c == y ? 1.f : 0.f)) * invB;
+    dot += p * dp;
+  }
+  dot = wave_sum(dot);
+  for (int c = lane; c < C; c += 64) {
+    const float p = lg[c];
+    const float dp = (__expf(p) / z2 - (c == y ? 1.f : 0.f)) * invB;
+    dlogits[(long)b * C + c] = p * (dp - dot);
+  }
+  if (lane == 0) atomicAdd(loss, (logf(z2) - lg[y]) * invB);
+}
+
+// dF[r] = (dn - n (n.dn)) / norm[r],  dn[k] = s * sum_c dlog(r, c) * other[c][k] (+ dn_ext)
+// dlog(r, c) = dlogits[r*sr + c*sc]
+__global__ void __launch_bounds__(256)
+head_feat_grad_kernel(int R, int Co, int E, const float* __restrict__ dlogits, long sr, long sc,
+                      const float* __restrict__ other_n, const float* __restrict__ self_n,
+                      const float* __restrict__ norms, const float* __restrict__ logit_scale,
+                      const float* __restrict__ dn_ext, float* __restrict__ dF) {
+  __shared__ float red[4];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float s = __expf(*logit_scale);
+  float dn[4] = {0.f, 0.f, 0.f, 0.f};  // E <= 1024
+  for (int c = 0; c < Co; ++c) {
+    const float d = dlogits[(long)r * sr + (long)c * sc];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = tid + i * 256;
+      if (k < E) dn[i] += d * other_n[(long)c * E + k];
+    }
+  }
+  float part = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = tid + i * 256;
+    if (k < E) {
+      dn[i] *= s;
+      if (dn_ext) dn[i] += dn_ext[(long)r * E + k];
+      part += dn[i] * self_n[(long)r * E + k];
+    }
+  }
+  part = wave_sum(part);
+  if ((tid & 63) == 0) red[tid >> 6] = part;
+  __syncthreads();
+  const float nd = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.0f / norms[r];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = tid + i * 256;
+    if (k < E) dF[(long)r * E + k] = (dn[i] - self_n[(long)r * E + k] * nd) * inv;
+  }
+}
+
+
+// logits[b][c] = exp(logit_scale) * img_n[b] . txt_n[c]; probs = softmax(logits) (optional)
+__global__ void __launch_bounds__(256)
+head_logits_kernel(int B, int C, int E, const float* __restrict__ img_n,
+                   const float* __restrict__ txt_n, const float* __restrict__ logit_scale,
+                   float* __restrict__ logits, float* __restrict__ probs) {
+  extern __shared__ float sh[];
+  float* irow = sh;
+  float* lg = sh + E;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float s = __expf(*logit_scale);
+  for (int k = tid; k < E; k += 256) irow[k] = img_n[(long)b * E + k];
+  __syncthreads();
+  for (int c = w; c < C; c += 4) {
+    float d = 0.f;
+    for (int k = lane; k < E; k += 64) d += irow[k] * txt_n[(long)c * E + k];
+    d = wave_sum(d);
+    if (lane == 0) {
+      lg[c] = s * d;
+      logits[(long)b * C + c] = s * d;
+    }
+  }
+  __syncthreads();
+  if (w != 0 || probs == nullptr) return;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, lg[c]);
+  m = wave_max(m);
+  float z = 0.f;
+  for (int c = lane; c < C; c += 64) z += __expf(lg[c] - m);
+  z = wave_sum(z);
+  for (int c = lane; c < C; c += 64) probs[(long)b * C + c] = __expf(lg[c] - m) / z;
+}
+
+// dlogits = p * (dp - sum_c p*dp), one wave per row
+__global__ void __launch_bounds__(64)
+softmax_bwd_kernel(int B, int C, const float* __restrict__ p, const float* __restrict__ dp,
+                   float* __restrict__ dl) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  float dot = 0.f;
+  for (int c = lane; c < C; c += 64) dot += p[(long)b * C + c] * dp[(long)b * C + c];
+  dot = wave_sum(dot);
+  for (int c = lane; c < C; c += 64)
+    dl[(long)b * C + c] = p[(long)b * C + c] * (dp[(long)b * C + c] - dot);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lc_l2norm_rows(hipStream_t st, int R, int E, const float* f, long ldf, float* out, float* norms) {
+  LC_CHECK_ARG(R > 0 && E > 0 && ldf >= E);
+  hipLaunchKernelGGL(l2norm_kernel, dim3(R), dim3(64), 0, st, R, E, f, ldf, out, norms);
+  LC_LAUNCH_RET();
+}
+
+int lc_clip_head(hipStream_t st, int B, int C, int E, const float* img_n, const float* txt_n,
+                 const float* logit_scale, const int64_t* labels, float* probs, float* dlogits,
+                 float* loss) {
+  LC_CHECK_ARG(B > 0 && C > 0 && C <= 8192 && E > 0 && E <= 1024);
+  const size_t shm = (size_t)(E + C) * sizeof(float);
+  hipLaunchKernelGGL(head_rows_kernel, dim3(B), dim3(256), shm, st, B, C, E, img_n, txt_n,
+                     logit_scale, labels, probs, dlogits, loss);
+  LC_LAUNCH_RET();
+}
+
+int lc_head_feat_grad(hipStream_t st, int R, int Co, int E, const float* dlogits, long sr, long sc,
+                      const float* other_n, const float* self_n, const float* norms,
+                      const float* logit_scale, const float* dn_ext, float* dF) {
+  LC_CHECK_ARG(R > 0 && Co > 0 && E > 0 && E <= 1024);
+  hipLaunchKernelGGL(head_feat_grad_kernel, dim3(R), dim3(256), 0, st, R, Co, E, dlogits, sr, sc,
+                     other_n, self_n, norms, logit_scale, dn_ext, dF);
+  LC_LAUNCH_RET();
+}
+
+int lc_head_logits(hipStream_t st, int B, int C, int E, const float* img_n, const float* txt_n,
+                   const float* logit_scale, float* logits, float* probs) {
+  LC_CHECK_ARG(B > 0 && C > 0 && C <= 8192 && E > 0 && E <= 1024);
+  const size_t shm = (size_t)(E + C) * sizeof(float);
+  hipLaunchKernelGGL(head_logits_kernel, dim3(B), dim3(256), shm, st, B, C, E, img_n, txt_n,
+                     logit_scale, logits, probs);
+  LC_LAUNCH_RET();
+}
+
+int lc_softmax_bwd_rows(hipStream_t st, int B, int C, const float* probs, const float* dprobs,
+                        float* dlogits) {
+  LC_CHECK_ARG(B > 0 && C > 0);
+  hipLaunchKernelGGL(softmax_bwd_kernel, dim3(B), dim3(64), 0, st, B, C, probs, dprobs, dlogits);
+  LC_LAUNCH_RET();
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) CLIP PEFT kernels.
+// Wave = 64 lanes; MFMA = v_mfma_f32_16x16x32_bf16 (A/B: 8 bf16 per lane, C/D: 4 f32 per lane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "lc_clip.h"
+
+typedef uint16_t bf16_t;  // raw bf16 bits in global memory
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LC_DEV __device__ __forceinline__
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+#define GLB_PTR(p) ((const __attribute__((address_space(1))) void*)(p))
+
+LC_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+LC_DEV float bf2f_s(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
+
+// fp32 -> bf16, round to nearest even; lowers to v_cvt_pk_bf16_f32 (NaN-preserving).
+LC_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+LC_DEV uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Async 16-byte global -> LDS copy; LDS destination = wave-uniform base + lane * 16.
+LC_DEV void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+
+LC_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+LC_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+LC_DEV float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+LC_DEV float quick_gelu_grad(float x) {
+  float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  return s + 1.702f * x * s * (1.0f - s);
+}
+
+// Counter-based hash RNG (splitmix-style) for adapter dropout masks: mask(seed, index) is a
+// pure function, so backward regenerates the forward's mask without storing it.
+LC_DEV uint32_t lc_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+
+
+#define LC_CHECK_ARG(cond) \
+  do {                     \
+    if (!(cond)) return LC_EINVAL; \
+  } while (0)
+
+#define LC_LAUNCH_RET()                                   \
+  do {                                                    \
+    hipError_t _e = hipGetLastError();                    \
+    return _e == hipSuccess ? LC_OK : LC_ELAUNCH;         \
+  } while (0)

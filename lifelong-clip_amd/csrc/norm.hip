@@ -1,0 +1,304 @@
+// Row-local kernels: LayerNorm fwd/bwd (models/clip/model.py:194-200, fp32 statistics,
+// eps 1e-5), ViT patch im2col + token assembly (model.py:756-764), text token embedding
+// (model.py:943-946) and EOT row selection (model.py:953-954).
+// One wave per row; rows are independent, so the grid is rows/4 workgroups of 4 waves. All
+// global traffic is 16 B per lane where the row width allows (D % 256 == 0: 768, 512, 1024).
+#include "lc_common.h"
+
+namespace {
+
+template <int V>  // V = D / 64 elements per lane
+struct RowBuf {
+  float v[V];
+};
+
+// Load a row of D = 64*V floats: lane holds elements {lane*4 + 256*i + j} when V % 4 == 0,
+// else {lane + 64*i}. Both layouts are used consistently for params and outputs.
+template <int V>
+LC_DEV void load_row_f32(const float* __restrict__ p, int lane, float (&v)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i) {
+      float4 t = *reinterpret_cast<const float4*>(p + i * 256 + lane * 4);
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = p[i * 64 + lane];
+  }
+}
+template <int V>
+LC_DEV void load_row_bf16(const bf16_t* __restrict__ p, int lane, float (&v)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i) {
+      uint2 t = *reinterpret_cast<const uint2*>(p + i * 256 + lane * 4);
+      v[4 * i] = bf2f(t.x & 0xffff); v[4 * i + 1] = bf2f(t.x >> 16);
+      v[4 * i + 2] = bf2f(t.y & 0xffff); v[4 * i + 3] = bf2f(t.y >> 16);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = bf2f(p[i * 64 + lane]);
+  }
+}
+template <int V>
+LC_DEV void store_row_f32(float* __restrict__ p, int lane, const float (&v)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i)
+      *reinterpret_cast<float4*>(p + i * 256 + lane * 4) =
+          make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i * 64 + lane] = v[i];
+  }
+}
+template <int V>
+LC_DEV void store_row_bf16(bf16_t* __restrict__ p, int lane, const float (&v)[V]) {
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i)
+      *reinterpret_cast<uint2*>(p + i * 256 + lane * 4) =
+          uint2{pack2bf(v[4 * i], v[4 * i + 1]), pack2bf(v[4 * i + 2], v[4 * i + 3])};
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i * 64 + lane] = f2bf(v[i]);
+  }
+}
+
+template <int V>
+__global__ void __launch_bounds__(256)
+ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __restrict__ row_idx,
+              const float* __restrict__ gamma, const float* __restrict__ beta, void* __restrict__ y,
+              int y_f32, long ldy, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int D = V * 64;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const long src = row_idx ? (long)row_idx[row] : (long)row;
+  float v[V];
+  load_row_f32<V>(x + src * ldx, lane, v);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) s += v[i];
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    v[i] -= mean;
+    q += v[i] * v[i];
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+  float gm[V], bt[V];
+  load_row_f32<V>(gamma, lane, gm);
+  load_row_f32<V>(beta, lane, bt);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = v[i] * rstd * gm[i] + bt[i];
+  if (y_f32) store_row_f32<V>((float*)y + (long)row * ldy, lane, v);
+  else store_row_bf16<V>((bf16_t*)y + (long)row * ldy, lane, v);
+  if (lane == 0 && mean_out) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; total = dres + dx.
+template <int V>
+__global__ void __launch_bounds__(256)
+ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
+              const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+              const float* __restrict__ rstd, const float* __restrict__ gamma,
+              const float* __restrict__ dres, float* __restrict__ dx, bf16_t* __restrict__ dxb,
+              long ldo, const int* __restrict__ row_idx) {
+  constexpr int D = V * 64;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const long xr = row_idx ? (long)row_idx[row] : (long)row;
+  float g[V], xv[V], gm[V];
+  if (dy_f32) load_row_f32<V>((const float*)dy + (long)row * ldy, lane, g);
+  else load_row_bf16<V>((const bf16_t*)dy + (long)row * ldy, lane, g);
+  load_row_f32<V>(x + xr * ldx, lane, xv);
+  load_row_f32<V>(gamma, lane, gm);
+  const float mu = mean[row], rs = rstd[row];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    xv[i] = (xv[i] - mu) * rs;
+    g[i] *= gm[i];
+    s1 += g[i];
+    s2 += g[i] * xv[i];
+  }
+  s1 = wave_sum(s1) * (1.0f / D);
+  s2 = wave_sum(s2) * (1.0f / D);
+  float out[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) out[i] = rs * (g[i] - s1 - xv[i] * s2);
+  if (dres) {
+    float r[V];
+    load_row_f32<V>(dres + xr * ldo, lane, r);
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] += r[i];
+  }
+  store_row_f32<V>(dx + xr * ldo, lane, out);
+  if (dxb) store_row_bf16<V>(dxb + xr * ldo, lane, out);
+}
+
+// im2col for conv1 (k = s = P): out[(n*g*g + py*g + px)][c*P*P + ky*P + kx] = img[n][c][py*P+ky][px*P+kx]
+__global__ void patchify_kernel(int n_img, int res, int P, const float* __restrict__ img,
+                                bf16_t* __restrict__ out) {
+  const int g = res / P;
+  const int cols = 3 * P * P;
+  const long total8 = (long)n_img * g * g * cols / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8;
+       e += (long)gridDim.x * blockDim.x) {
+    const long flat = e * 8;
+    const long row = flat / cols;
+    const int col = (int)(flat % cols);
+    const int n = (int)(row / (g * g)), pp = (int)(row % (g * g));
+    const int py = pp / g, px = pp % g;
+    const int c = col / (P * P), rem = col % (P * P), ky = rem / P, kx = rem % P;
+    const float* src = img + (((long)n * 3 + c) * res + (py * P + ky)) * res + px * P + kx;
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 b = *reinterpret_cast<const float4*>(src + 4);
+    *reinterpret_cast<uint4*>(out + flat) =
+        uint4{pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w)};
+  }
+}
+
+// x[n][0] = cls + pos[0]; x[n][1+p] = patch[n*np + p] + pos[1+p]   (model.py:759-764)
+__global__ void vit_assemble_kernel(int n_img, int np, int D, const float* __restrict__ patch,
+                                    const float* __restrict__ cls, const float* __restrict__ pos,
+                                    float* __restrict__ x) {
+  const int L = np + 1;
+  const long total4 = (long)n_img * L * D / 4;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total4;
+       e += (long)gridDim.x * blockDim.x) {
+    const long flat = e * 4;
+    const long row = flat / D;
+    const int col = (int)(flat % D);
+    const int n = (int)(row / L), t = (int)(row % L);
+    float4 v = t == 0 ? *reinterpret_cast<const float4*>(cls + col)
+                      : *reinterpret_cast<const float4*>(patch + ((long)n * np + t - 1) * D + col);
+    const float4 p = *reinterpret_cast<const float4*>(pos + (long)t * D + col);
+    *reinterpret_cast<float4*>(x + flat) = make_float4(v.x + p.x, v.y + p.y, v.z + p.z, v.w + p.w);
+  }
+}
+
+// x[c][t] = tok_emb[tokens[c][t]] + pos[t]   (model.py:943-946)
+__global__ void text_embed_kernel(int C, int L, int D, const int64_t* __restrict__ tokens,
+                                  const float* __restrict__ emb, const float* __restrict__ pos,
+                                  float* __restrict__ x) {
+  const long total4 = (long)C * L * D / 4;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total4;
+       e += (long)gridDim.x * blockDim.x) {
+    const long flat = e * 4;
+    const long row = flat / D;
+    const int col = (int)(flat % D);
+    const int t = (int)(row % L);
+    const long tok = tokens[row];
+    const float4 a = *reinterpret_cast<const float4*>(emb + tok * D + col);
+    const float4 p = *reinterpret_cast<const float4*>(pos + (long)t * D + col);
+    *reinterpret_cast<float4*>(x + flat) = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+  }
+}
+
+// row_idx[c] = c*L + argmax_t tokens[c][t]  (first maximum, as torch.argmax)
+__global__ void eot_rows_kernel(int C, int L, const int64_t* __restrict__ tokens,
+                                int* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  int best = 0;
+  int64_t bv = tokens[(long)c * L];
+  for (int t = 1; t < L; ++t) {
+    int64_t v = tokens[(long)c * L + t];
+    if (v > bv) { bv = v; best = t; }
+  }
+  out[c] = c * L + best;
+}
+
+int grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  if (g > 8192) g = 8192;
+  return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lc_layernorm_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, const int* row_idx,
+                     const float* gamma, const float* beta, void* y, int y_f32, long ldy,
+                     float* mean, float* rstd) {
+  LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
+  if (rows == 0) return LC_OK;
+  dim3 grid((rows + 3) / 4), block(256);
+  switch (D / 64) {
+#define LC_LN_F(V)                                                                               \
+  case V:                                                                                       \
+    hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, block, 0, st, rows, x, ldx, row_idx, gamma, beta, \
+                       y, y_f32, ldy, mean, rstd);                                              \
+    break;
+    LC_LN_F(1) LC_LN_F(2) LC_LN_F(4) LC_LN_F(8) LC_LN_F(12) LC_LN_F(16)
+    default:
+      return LC_EINVAL;
+#undef LC_LN_F
+  }
+  LC_LAUNCH_RET();
+}
+
+int lc_layernorm_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
+                     const float* x, long ldx, const float* mean, const float* rstd,
+                     const float* gamma, const float* dres, float* dx, void* dx_bf16, long ldo,
+                     const int* row_idx) {
+  LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
+  if (rows == 0) return LC_OK;
+  dim3 grid((rows + 3) / 4), block(256);
+  switch (D / 64) {
+#define LC_LN_B(V)                                                                              \
+  case V:                                                                                      \
+    hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy, x, ldx,    \
+                       mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16, ldo, row_idx);           \
+    break;
+    LC_LN_B(1) LC_LN_B(2) LC_LN_B(4) LC_LN_B(8) LC_LN_B(12) LC_LN_B(16)
+    default:
+      return LC_EINVAL;
+#undef LC_LN_B
+  }
+  LC_LAUNCH_RET();
+}
+
+int lc_patchify(hipStream_t st, int n_img, int res, int patch, const float* img, void* out) {
+  LC_CHECK_ARG(n_img > 0 && patch % 8 == 0 && res % patch == 0);
+  const long work = (long)n_img * res * res * 3 / 8;
+  hipLaunchKernelGGL(patchify_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, n_img, res,
+                     patch, img, (bf16_t*)out);
+  LC_LAUNCH_RET();
+}
+
+int lc_vit_assemble(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
+                    const float* cls, const float* pos, float* x) {
+  LC_CHECK_ARG(n_img > 0 && D % 4 == 0);
+  const long work = (long)n_img * (n_patch + 1) * D / 4;
+  hipLaunchKernelGGL(vit_assemble_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, n_img,
+                     n_patch, D, patch, cls, pos, x);
+  LC_LAUNCH_RET();
+}
+
+int lc_text_embed(hipStream_t st, int C, int L, int D, const int64_t* tokens, const float* emb,
+                  const float* pos, float* x) {
+  LC_CHECK_ARG(C > 0 && L > 0 && D % 4 == 0);
+  const long work = (long)C * L * D / 4;
+  hipLaunchKernelGGL(text_embed_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, C, L, D,
+                     tokens, emb, pos, x);
+  LC_LAUNCH_RET();
+}
+
+int lc_eot_rows(hipStream_t st, int C, int L, const int64_t* tokens, int* row_idx) {
+  LC_CHECK_ARG(C > 0 && L > 0);
+  hipLaunchKernelGGL(eot_rows_kernel, dim3((C + 255) / 256), dim3(256), 0, st, C, L, tokens,
+                     row_idx);
+  LC_LAUNCH_RET();
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+"""ctypes binding of liblcclip.so (the C ABI declared in include/lc_clip.h).
+
+The product path has no fallback: if the library is missing or a GPU is not present, every
+op raises. Tensors cross the boundary as raw device pointers + sizes; the stream is torch's
+current HIP stream on the tensor's device.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_long, c_ulonglong, c_void_p
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblcclip.so")
+
+P = c_void_p
+# name -> argtypes (restype is always c_int); mirrors include/lc_clip.h
+SIGNATURES = {
+    "lc_gemm_nt": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_float, P, c_long, P,
+                   c_long, P, c_long],
+    "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long],
+    "lc_layernorm_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_int, c_long, P, P],
+    "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
+    "lc_patchify": [P, c_int, c_int, c_int, P, P],
+    "lc_vit_assemble": [P, c_int, c_int, c_int, P, P, P, P],
+    "lc_text_embed": [P, c_int, c_int, c_int, P, P, P, P],
+    "lc_eot_rows": [P, c_int, c_int, P, P],
+    "lc_attn_fwd": [P, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int],
+    "lc_attn_bwd": [P, c_int, c_int, c_int, P, c_long, P, P, c_long, P, P, c_long, c_int],
+    "lc_cast_bf16": [P, c_long, P, P],
+    "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
+    "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
+    "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
+                       c_long, P],
+    "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long, P, P],
+    "lc_check_finite": [P, c_long, P, P],
+    "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P],
+    "lc_l2norm_rows": [P, c_int, c_int, P, c_long, P, P],
+    "lc_clip_head": [P, c_int, c_int, c_int, P, P, P, P, P, P, P],
+    "lc_head_logits": [P, c_int, c_int, c_int, P, P, P, P, P],
+    "lc_softmax_bwd_rows": [P, c_int, c_int, P, P, P],
+    "lc_head_feat_grad": [P, c_int, c_int, c_int, P, c_long, c_long, P, P, P, P, P, P],
+}
+
+_lib = None
+
+
+class LcError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load liblcclip.so and declare every entry point. Raises if anything is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LcError(f"liblcclip.so not built at {path}; run `python __graft_entry__.py build` "
+                      "(there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is missing
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    _lib = lib
+    return lib
+
+
+def exported_symbols(path: str = LIB_PATH):
+    lib = ctypes.CDLL(path)
+    return {n for n in SIGNATURES if hasattr(lib, n)}
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    if not t.is_cuda:
+        raise LcError("lcclip ops require tensors on a HIP device (no CPU fallback)")
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        kind = {-1: "invalid argument / shape", -2: "kernel launch failed"}.get(rc, "error")
+        raise LcError(f"{name} returned {rc} ({kind})")

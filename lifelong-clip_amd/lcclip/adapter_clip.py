@@ -1,0 +1,112 @@
+"""AdapterCLIP — drop-in for models/adapter_clip.py:14-137 of qcNPU/LifeLong-CLIP.
+
+Same constructor arguments, attributes (.model, .dtype, .text_tokens, .current_class_names,
+.prompt_template) and forward contract: forward(image, text_tokens=None) ->
+(probs [B,C], image_features [B,E], text_features [C,E]) with probs = softmax(logits)
+(adapter_clip.py:94-100). `.module` returns self so the reference trainer's
+`self.custom_clip.module...` calls work on one GPU (Q4).
+
+Tokenisation (the CLIP BPE, models/clip/tokenizer.py) is a CPU producer of int64 ids and is out
+of this build's scope: pass `tokenizer=` (a callable text -> list[int] without
+SOT/EOT) to use class names, or hand set_token()/forward() precomputed token ids.
+"""
+from __future__ import annotations
+
+from typing import List, Union
+
+import torch
+import torch.nn as nn
+
+from . import autograd as lc_autograd
+from . import clip_loader
+
+SOT_TOKEN = 49406
+EOT_TOKEN = 49407
+
+
+class AdapterCLIP(nn.Module):
+    def __init__(self, model_name, peft_method="adapter", peft_encoder="both", device=None,
+                 tokenizer=None, arch_overrides=None):
+        super().__init__()
+        self.device = device
+        design_details = {
+            "method": peft_method,
+            "peft_encoder": peft_encoder,
+            "ffn_num": 64,
+            "lora_alpha": 1,
+            "lora_r": 4,
+        }
+        self.model = clip_loader.load(model_name, device=device, jit=False,
+                                      design_details=design_details, arch_overrides=arch_overrides)
+        self.text_tokens = None
+        self.current_class_names = []
+        self.dtype = self.model.dtype
+        self.prompt_template = "a bad photo of a {}."
+        self._tokenizer = tokenizer
+
+    @property
+    def module(self):
+        return self
+
+    def tokenize(self, texts: Union[str, List[str]], context_length: int = 77) -> torch.LongTensor:
+        """adapter_clip.py:108-137 (requires a tokenizer callable)."""
+        if self._tokenizer is None:
+            raise RuntimeError("no BPE tokenizer configured; pass tokenizer= or token ids")
+        if isinstance(texts, str):
+            texts = [texts]
+        all_tokens = [[SOT_TOKEN] + list(self._tokenizer(t)) + [EOT_TOKEN] for t in texts]
+        result = torch.zeros(len(all_tokens), context_length, dtype=torch.long)
+        for i, tokens in enumerate(all_tokens):
+            tokens = tokens[:context_length]
+            result[i, :len(tokens)] = torch.tensor(tokens)
+        return result
+
+    def labels_tokenize(self, labels, context_length: int = 77) -> torch.LongTensor:
+        """adapter_clip.py:43-74: prompt template applied to each class name."""
+        if isinstance(labels, str):
+            labels = [labels]
+        return self.tokenize([self.prompt_template.format(c) for c in labels], context_length).to(
+            self._param_device())
+
+    def _param_device(self):
+        return self.model.logit_scale.device
+
+    def encode_image(self, image):
+        """adapter_clip.py:76-79 (L2-normalised image features)."""
+        return lc_autograd.l2norm_apply(self.model.encode_image(image))
+
+    def update_class_names(self, new_class_names):
+        """adapter_clip.py:81-92 (appends unseen names; returns None as the reference does)."""
+        for c in new_class_names:
+            if c not in self.current_class_names:
+                self.current_class_names.append(c)
+        return None
+
+    def forward(self, image, text_tokens=None):
+        if text_tokens is None:
+            text_tokens = self.text_tokens
+        img_f = self.model.encode_image(image)
+        txt_f = self.model.encode_text(text_tokens)
+        probs, image_features, text_features = lc_autograd.head_apply(
+            img_f, txt_f, self.model.logit_scale, probs=True)
+        return probs, image_features, text_features
+
+    def set_token(self, classnames_or_tokens):
+        """adapter_clip.py:102-104; accepts class names (needs a tokenizer) or token ids."""
+        if isinstance(classnames_or_tokens, torch.Tensor):
+            tokens = classnames_or_tokens.to(self._param_device(), torch.long)
+        else:
+            tokens = self.labels_tokenize(classnames_or_tokens)
+        if "text_tokens" in self._buffers:
+            del self._buffers["text_tokens"]
+        elif hasattr(self, "text_tokens"):
+            del self.text_tokens
+        self.register_buffer("text_tokens", tokens)
+
+
+def freeze_backbone(model: nn.Module):
+    """methods/adapter_clip.py:117-119: only '*adaptmlp*' / '*lora*' parameters stay trainable."""
+    for k, v in model.named_parameters():
+        if "adaptmlp" not in k and "lora" not in k:
+            v.requires_grad = False
+    return model

@@ -1,0 +1,148 @@
+"""torch.autograd.Function wrappers that connect the fused tower engines to autograd.
+
+Only the PEFT parameters (LoRA A/B, adapter weights/biases) are passed as Function inputs, so
+autograd routes their gradients; the frozen backbone is read from the modules directly.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .ops import BF16, F32
+
+
+def _check_frozen(stack):
+    if torch.is_grad_enabled():
+        for p in stack.backbone_params():
+            if p.requires_grad:
+                raise RuntimeError(
+                    "lcclip computes PEFT gradients only: freeze the backbone first (the "
+                    "reference does in online_before_task, methods/adapter_clip.py:115-119; "
+                    "see lcclip.freeze_backbone)")
+
+
+class _TowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tower, inp, training, save, *params):
+        f, c = tower.forward(inp, save=save, training=training)
+        ctx.tower = tower
+        ctx.saved_ctx = c
+        ctx.params = tower.stack.trainable_params()
+        return f
+
+    @staticmethod
+    def backward(ctx, df):
+        if ctx.saved_ctx is None:
+            raise RuntimeError("tower forward ran without saving activations")
+        grads = {p: torch.zeros(p.shape, dtype=F32, device=p.device) for p in ctx.params}
+        ctx.tower.backward(ctx.saved_ctx, df.contiguous().float(), grads)
+        ctx.saved_ctx = None
+        return (None, None, None, None, *[grads[p] for p in ctx.params])
+
+
+def tower_apply(tower, transformer, inp, training):
+    stack = tower.stack
+    _check_frozen(stack)
+    params = stack.trainable_params()
+    save = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+    return _TowerFn.apply(tower, inp, bool(training), save, *params)
+
+
+class _StackFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, stack, x, n_seq, L, training, save, *params):
+        y, saved = stack.forward(x, n_seq, L, save=save, training=training)
+        ctx.stack, ctx.saved_list, ctx.n_seq, ctx.L = stack, saved, n_seq, L
+        ctx.params = stack.trainable_params()
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous().float().clone()
+        dyb = torch.empty(dy.shape, dtype=BF16, device=dy.device)
+        ops.cast_bf16(dy, dyb)
+        grads = {p: torch.zeros(p.shape, dtype=F32, device=p.device) for p in ctx.params}
+        dx, _ = ctx.stack.backward(ctx.saved_list, dy, dyb, grads, ctx.n_seq, ctx.L)
+        ctx.saved_list = None
+        return (None, dx, None, None, None, None, *[grads[p] for p in ctx.params])
+
+
+def stack_apply(transformer, x2d, n_seq, L):
+    stack = transformer.engine
+    _check_frozen(stack)
+    params = stack.trainable_params()
+    save = torch.is_grad_enabled() and (x2d.requires_grad or any(p.requires_grad for p in params))
+    return _StackFn.apply(stack, x2d, n_seq, L, bool(transformer.training), save, *params)
+
+
+class _HeadFn(torch.autograd.Function):
+    """model.py:966-974 (+ models/adapter_clip.py:99 softmax when probs=True)."""
+
+    @staticmethod
+    def forward(ctx, img_f, txt_f, logit_scale, probs):
+        img_f = img_f.contiguous().float()
+        txt_f = txt_f.contiguous().float()
+        B, E = img_f.shape
+        C = txt_f.shape[0]
+        dev = img_f.device
+        img_n = torch.empty_like(img_f)
+        txt_n = torch.empty_like(txt_f)
+        ni = torch.empty(B, dtype=F32, device=dev)
+        nt = torch.empty(C, dtype=F32, device=dev)
+        ops.l2norm_rows(img_f, img_n, ni)
+        ops.l2norm_rows(txt_f, txt_n, nt)
+        logits = torch.empty(B, C, dtype=F32, device=dev)
+        pr = torch.empty(B, C, dtype=F32, device=dev) if probs else None
+        ls = logit_scale.detach().reshape(1).float().contiguous()
+        ops.head_logits(img_n, txt_n, ls, logits, pr)
+        ctx.save_for_backward(img_n, txt_n, ni, nt, ls, pr if probs else logits)
+        ctx.probs = probs
+        out = pr if probs else logits
+        return out, img_n, txt_n
+
+    @staticmethod
+    def backward(ctx, d_out, d_img_n, d_txt_n):
+        img_n, txt_n, ni, nt, ls, pr = ctx.saved_tensors
+        B, C = d_out.shape
+        d_out = d_out.contiguous().float()
+        if ctx.probs:
+            dlog = torch.empty_like(d_out)
+            ops.softmax_bwd_rows(pr, d_out, dlog)
+        else:
+            dlog = d_out
+        d_img = torch.empty_like(img_n)
+        d_txt = torch.empty_like(txt_n)
+        ops.head_feat_grad(dlog, C, 1, txt_n, img_n, ni, ls, d_img,
+                           None if d_img_n is None else d_img_n.contiguous().float())
+        ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, ls, d_txt,
+                           None if d_txt_n is None else d_txt_n.contiguous().float())
+        return d_img, d_txt, None, None
+
+
+def head_apply(img_f, txt_f, logit_scale, probs: bool):
+    return _HeadFn.apply(img_f, txt_f, logit_scale, probs)
+
+
+class _L2NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f):
+        f = f.contiguous().float()
+        out = torch.empty_like(f)
+        nrm = torch.empty(f.shape[0], dtype=F32, device=f.device)
+        ops.l2norm_rows(f, out, nrm)
+        ctx.save_for_backward(out, nrm)
+        return out
+
+    @staticmethod
+    def backward(ctx, dn):
+        out, nrm = ctx.saved_tensors
+        # dF = (dn - n (n.dn)) / |f|: the head-gradient kernel with no logit term (Co = 1, dlog = 0)
+        zero = torch.zeros(out.shape[0], 1, dtype=F32, device=out.device)
+        one = torch.zeros(1, dtype=F32, device=out.device)
+        dF = torch.empty_like(out)
+        ops.head_feat_grad(zero, 1, 1, out[:1], out, nrm, one, dF, dn.contiguous().float())
+        return dF
+
+
+def l2norm_apply(f):
+    return _L2NormFn.apply(f)

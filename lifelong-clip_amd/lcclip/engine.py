@@ -1,0 +1,375 @@
+"""Tower engines: the fused forward/backward of a stack of CLIP residual blocks and of the two
+encoders, entirely through liblcclip.so kernels.
+
+Reference semantics (qcNPU/LifeLong-CLIP):
+  block        models/clip/model.py:233-236 (vanilla / LoRA), :439-442 (adapter, Q6)
+  LoRA MHA     models/clip/lora.py:832-1074
+  adapter      models/clip/adapter.py:53-72
+  image tower  models/clip/model.py:755-787 (Q1: blocks called as blk(x))
+  text tower   models/clip/model.py:941-956
+
+Data layout in HBM (rows = sequence * L tokens, batch-major; the reference's sequence-first
+layout is internal and not observable):
+  residual stream   f32  [rows, D]   one buffer per sub-block output (kept for LN backward)
+  LN outputs        bf16 [rows, D]   transient unless a LoRA in-proj needs them for dA
+  qkv               bf16 [rows, 3D]  kept (attention backward)
+  attention out O   bf16 [rows, D]   kept; lse f32 [seq*H, L]
+  MLP pre-activation bf16 [rows, 4D] kept (QuickGELU backward); GELU output transient
+  adapter input z   bf16 [rows, D], bottleneck h bf16 [rows, 64]  kept
+Frozen weights are staged once as bf16 in both [out,in] and [in,out] layouts (forward and dX
+GEMMs are both A @ B^T); LoRA blocks re-merge W + s*B@A into those buffers each step.
+The backbone is frozen: backward produces input gradients and PEFT parameter gradients only.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+
+from . import ops
+from .ops import BF16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_BWD, EPI_RESID
+
+_seed_counter = itertools.count(1)
+
+
+def _empty(shape, dtype, dev):
+    return torch.empty(shape, dtype=dtype, device=dev)
+
+
+def _key(*tensors):
+    return tuple((t.data_ptr(), t._version) for t in tensors if t is not None)
+
+
+class StagedBlock:
+    """bf16 device copies of one block's GEMM weights (both layouts)."""
+
+    def __init__(self):
+        self.frozen_key = None
+        self.peft_key = None
+
+
+class BlockStack:
+    """Engine for `Transformer.resblocks` (model.py:639-686): a list of block modules sharing
+    width, heads, mask and PEFT variant."""
+
+    def __init__(self, blocks, n_head: int, causal: bool, variant: str):
+        self.blocks = list(blocks)
+        self.n_head = n_head
+        self.causal = bool(causal)
+        self.variant = variant  # 'vanilla' | 'lora' | 'adapter'
+        self.staged = [StagedBlock() for _ in self.blocks]
+
+    # ------------------------------------------------------------------ weight staging
+    def trainable_params(self):
+        out = []
+        for b in self.blocks:
+            out.extend(b.peft_parameters())
+        return out
+
+    def backbone_params(self):
+        out = []
+        for b in self.blocks:
+            out.extend(b.backbone_parameters())
+        return out
+
+    def stage(self):
+        for blk, st in zip(self.blocks, self.staged):
+            attn, mlp = blk.attn, blk.mlp
+            fkey = _key(attn.in_proj_weight, attn.out_proj.weight, mlp.c_fc.weight, mlp.c_proj.weight)
+            if fkey != st.frozen_key:
+                dev = attn.in_proj_weight.device
+                D = attn.in_proj_weight.shape[1]
+                st.wqkv = _empty((3 * D, D), BF16, dev)
+                st.wqkvT = _empty((D, 3 * D), BF16, dev)
+                st.wo = _empty((D, D), BF16, dev)
+                st.woT = _empty((D, D), BF16, dev)
+                st.wfc = _empty((4 * D, D), BF16, dev)
+                st.wfcT = _empty((D, 4 * D), BF16, dev)
+                st.wpr = _empty((D, 4 * D), BF16, dev)
+                st.wprT = _empty((4 * D, D), BF16, dev)
+                ops.merge_weight(mlp.c_fc.weight.detach(), None, None, 0.0, st.wfc, st.wfcT)
+                ops.merge_weight(mlp.c_proj.weight.detach(), None, None, 0.0, st.wpr, st.wprT)
+                if self.variant != "lora":
+                    ops.merge_weight(attn.in_proj_weight.detach(), None, None, 0.0, st.wqkv, st.wqkvT)
+                    ops.merge_weight(attn.out_proj.weight.detach(), None, None, 0.0, st.wo, st.woT)
+                st.frozen_key = fkey
+                st.peft_key = None
+            if self.variant == "lora":
+                pkey = _key(attn.in_proj_weight_lora_A, attn.in_proj_weight_lora_B,
+                            attn.out_proj.lora_A, attn.out_proj.lora_B) + fkey
+                if pkey != st.peft_key:
+                    s = attn.scaling
+                    ops.merge_weight(attn.in_proj_weight.detach(), attn.in_proj_weight_lora_A.detach(),
+                                     attn.in_proj_weight_lora_B.detach(), s, st.wqkv, st.wqkvT)
+                    ops.merge_weight(attn.out_proj.weight.detach(), attn.out_proj.lora_A.detach(),
+                                     attn.out_proj.lora_B.detach(), s, st.wo, st.woT)
+                    st.peft_key = pkey
+            elif self.variant == "adapter":
+                ad = blk.adaptmlp
+                pkey = _key(ad.down_proj.weight, ad.up_proj.weight)
+                if pkey != st.peft_key:
+                    dev = ad.down_proj.weight.device
+                    D = ad.down_proj.weight.shape[1]
+                    H = ad.down_proj.weight.shape[0]
+                    st.wd = _empty((H, D), BF16, dev)
+                    st.wdT = _empty((D, H), BF16, dev)
+                    st.wu = _empty((D, H), BF16, dev)
+                    st.wuT = _empty((H, D), BF16, dev)
+                    ops.merge_weight(ad.down_proj.weight.detach(), None, None, 0.0, st.wd, st.wdT)
+                    ops.merge_weight(ad.up_proj.weight.detach(), None, None, 0.0, st.wu, st.wuT)
+                    st.peft_key = pkey
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False):
+        """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None)."""
+        self.stage()
+        M, D = x.shape
+        H = self.n_head
+        dev = x.device
+        tmp_h = _empty((M, D), BF16, dev)
+        tmp_g = _empty((M, 4 * D), BF16, dev)
+        tmp_pre = None if save else _empty((M, 4 * D), BF16, dev)
+        saved = [] if save else None
+        for blk, st in zip(self.blocks, self.staged):
+            s = {}
+            mean1 = _empty((M,), F32, dev)
+            rstd1 = _empty((M,), F32, dev)
+            h1 = _empty((M, D), BF16, dev) if (save and self.variant == "lora") else tmp_h
+            ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
+            qkv = _empty((M, 3 * D), BF16, dev)
+            ops.gemm_nt(h1, st.wqkv, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
+            O = _empty((M, D), BF16, dev)
+            lse = _empty((n_seq * H, L), F32, dev)
+            ops.attn_fwd(qkv, O, lse, n_seq, L, H, self.causal)
+            x_mid = _empty((M, D), F32, dev)
+            if self.variant == "adapter":
+                ad = blk.adaptmlp
+                keep = 1.0 - ad.dropout if (training and ad.dropout > 0) else 1.0
+                seed1 = next(_seed_counter) * 0x9E3779B1
+                z1 = _empty((M, D), BF16, dev)
+                ops.gemm_nt(O, st.wo, EPI_BF16, z1, bias=blk.attn.out_proj.bias)
+                hd1 = _empty((M, ad.down_size), BF16, dev)
+                ops.adapter_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale, keep,
+                                seed1, x, x_mid, hd1)
+                s.update(z1=z1, hd1=hd1, keep=keep)
+            else:
+                ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
+            mean2 = _empty((M,), F32, dev)
+            rstd2 = _empty((M,), F32, dev)
+            ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, tmp_h, mean2, rstd2)
+            pre = _empty((M, 4 * D), BF16, dev) if save else tmp_pre
+            ops.gemm_nt(tmp_h, st.wfc, EPI_GELU, pre, bias=blk.mlp.c_fc.bias, out1=tmp_g)
+            x_out = _empty((M, D), F32, dev)
+            if self.variant == "adapter":
+                ad = blk.adaptmlp
+                seed2 = next(_seed_counter) * 0x9E3779B1
+                z2 = _empty((M, D), BF16, dev)
+                ops.gemm_nt(tmp_g, st.wpr, EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
+                hd2 = _empty((M, ad.down_size), BF16, dev)
+                ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
+                                s["keep"], seed2, x_mid, x_out, hd2)
+                s.update(z2=z2, hd2=hd2)
+            else:
+                ops.gemm_nt(tmp_g, st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
+            if save:
+                s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
+                         mean2=mean2, rstd2=rstd2, pre=pre)
+                if self.variant == "lora":
+                    s["h1"] = h1
+                saved.append(s)
+            x = x_out
+        return x, saved
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, saved, dx, dxb, grads, n_seq: int, L: int):
+        """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
+        param -> f32 tensor (accumulated). Returns (dx, dxb) w.r.t. the stack input."""
+        M, D = dx.shape
+        H = self.n_head
+        dev = dx.device
+        da = _empty((M, 4 * D), BF16, dev)
+        dh = _empty((M, D), BF16, dev)
+        dO = _empty((M, D), BF16, dev)
+        dqkv = _empty((M, 3 * D), BF16, dev)
+        dz = _empty((M, D), BF16, dev) if self.variant == "adapter" else None
+        dx_mid = _empty((M, D), F32, dev)
+        dx_midb = _empty((M, D), BF16, dev)
+        dx_new = _empty((M, D), F32, dev)
+        dxb_new = _empty((M, D), BF16, dev)
+        for li in range(len(self.blocks) - 1, -1, -1):
+            blk, st, s = self.blocks[li], self.staged[li], saved[li]
+            # ---- MLP sub-block: x_out = x_mid + [A](c_proj(gelu(c_fc(ln_2(x_mid)))))
+            if self.variant == "adapter":
+                dY = self._adapter_bwd(blk, st, dxb, s["hd2"], s["z2"], s["keep"], dz, grads)
+            else:
+                dY = dxb
+            ops.gemm_nt(dY, st.wprT, EPI_GELU_BWD, da, aux=s["pre"])
+            ops.gemm_nt(da, st.wfcT, EPI_BF16, dh)
+            ops.layernorm_bwd(dh, s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight, dx_mid,
+                              dx_midb, dres=dx)
+            # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))
+            if self.variant == "adapter":
+                dY = self._adapter_bwd(blk, st, dx_midb, s["hd1"], s["z1"], s["keep"], dz, grads)
+            else:
+                dY = dx_midb
+            ops.gemm_nt(dY, st.woT, EPI_BF16, dO)
+            attn = blk.attn
+            if self.variant == "lora":
+                self._lora_grad(dY, s["O"], attn.out_proj.lora_A, attn.out_proj.lora_B,
+                                attn.scaling, grads)
+            ops.attn_bwd(s["qkv"], s["O"], dO, s["lse"], dqkv, n_seq, L, H, self.causal)
+            ops.gemm_nt(dqkv, st.wqkvT, EPI_BF16, dh)
+            if self.variant == "lora":
+                self._lora_grad(dqkv, s["h1"], attn.in_proj_weight_lora_A,
+                                attn.in_proj_weight_lora_B, attn.scaling, grads)
+            ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
+                              dxb_new, dres=dx_mid)
+            # ping-pong: the consumed output-gradient buffers are recycled for the next layer
+            dx, dx_new = dx_new, dx
+            dxb, dxb_new = dxb_new, dxb
+        return dx, dxb
+
+    @staticmethod
+    def _grad(grads, p):
+        g = grads.get(p)
+        if g is None:
+            raise KeyError("missing gradient buffer for a trainable parameter")
+        return g
+
+    def _adapter_bwd(self, blk, st, gout, h, z, keep, dz, grads):
+        ad = blk.adaptmlp
+        M = gout.shape[0]
+        dpre = _empty((M, ad.down_size), BF16, gout.device)
+        ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz,
+                        self._grad(grads, ad.down_proj.bias), self._grad(grads, ad.up_proj.bias))
+        ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale)
+        ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0)
+        return dz
+
+    def _lora_grad(self, dY, X, A, B, scaling, grads):
+        ops.lora_grad(dY, X, A.detach(), B.detach(), scaling, self._grad(grads, A),
+                      self._grad(grads, B))
+
+
+class ImageTower:
+    """VisualTransformer.forward (model.py:755-787) on the engine."""
+
+    def __init__(self, visual, stack: BlockStack):
+        self.visual = visual
+        self.stack = stack
+        self._key = None
+
+    def _stage(self):
+        v = self.visual
+        key = _key(v.conv1.weight, v.proj)
+        if key != self._key:
+            W = v.conv1.weight.shape[0]
+            dev = v.conv1.weight.device
+            self.conv_w = _empty((W, v.conv1.weight[0].numel()), BF16, dev)
+            ops.merge_weight(v.conv1.weight.detach().reshape(W, -1), None, None, 0.0, self.conv_w)
+            E = v.proj.shape[1]
+            self.projT = _empty((E, W), BF16, dev)      # forward: f = x @ proj  -> B = proj^T
+            self.proj = _empty((W, E), BF16, dev)       # backward: dx = df @ proj^T -> B = proj
+            ops.merge_weight(v.proj.detach(), None, None, 0.0, self.proj, self.projT)
+            self._key = key
+
+    def forward(self, img, save: bool, training: bool = False):
+        v = self.visual
+        self._stage()
+        dev = img.device
+        n = img.shape[0]
+        P = v.patch_size
+        g = v.input_resolution // P
+        npch = g * g
+        L = npch + 1
+        D = v.width
+        img = img.contiguous().to(F32)
+        patches = _empty((n * npch, 3 * P * P), BF16, dev)
+        ops.patchify(img, P, patches)
+        pe = _empty((n * npch, D), F32, dev)
+        ops.gemm_nt(patches, self.conv_w, EPI_F32, pe)
+        xa = _empty((n * L, D), F32, dev)
+        ops.vit_assemble(pe, v.class_embedding, v.positional_embedding, xa, n, npch)
+        x0 = _empty((n * L, D), F32, dev)
+        ops.layernorm_fwd(xa, v.ln_pre.weight, v.ln_pre.bias, x0)
+        x, saved = self.stack.forward(x0, n, L, save, training)
+        cls_idx = torch.arange(n, device=dev, dtype=torch.int32) * L
+        lnp = _empty((n, D), BF16, dev)
+        mean = _empty((n,), F32, dev)
+        rstd = _empty((n,), F32, dev)
+        ops.layernorm_fwd(x, v.ln_post.weight, v.ln_post.bias, lnp, mean, rstd, row_idx=cls_idx)
+        f = _empty((n, self.projT.shape[0]), F32, dev)
+        ops.gemm_nt(lnp, self.projT, EPI_F32, f)
+        ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L) if save else None
+        return f, ctx
+
+    def backward(self, ctx, df, grads):
+        v = self.visual
+        dev = df.device
+        n, L = ctx["n"], ctx["L"]
+        D = v.width
+        dfb = _empty(df.shape, BF16, dev)
+        ops.cast_bf16(df.contiguous(), dfb)
+        dln = _empty((n, D), F32, dev)
+        ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
+        dx = torch.zeros((n * L, D), dtype=F32, device=dev)
+        dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
+        ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
+                          row_idx=ctx["cls_idx"])
+        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L)
+
+
+class TextTower:
+    """CLIP.encode_text (model.py:941-956) on the engine."""
+
+    def __init__(self, clip, stack: BlockStack):
+        self.clip = clip
+        self.stack = stack
+        self._key = None
+
+    def _stage(self):
+        c = self.clip
+        key = _key(c.text_projection)
+        if key != self._key:
+            P = c.text_projection
+            dev = P.device
+            self.projT = _empty((P.shape[1], P.shape[0]), BF16, dev)
+            self.proj = _empty(tuple(P.shape), BF16, dev)
+            ops.merge_weight(P.detach(), None, None, 0.0, self.proj, self.projT)
+            self._key = key
+
+    def forward(self, tokens, save: bool, training: bool = False):
+        c = self.clip
+        self._stage()
+        dev = tokens.device
+        tokens = tokens.contiguous().to(torch.int64)
+        C, L = tokens.shape
+        D = c.transformer.width
+        x0 = _empty((C * L, D), F32, dev)
+        ops.text_embed(tokens, c.token_embedding.weight, c.positional_embedding, x0)
+        x, saved = self.stack.forward(x0, C, L, save, training)
+        eot = _empty((C,), torch.int32, dev)
+        ops.eot_rows(tokens, eot)
+        lnf = _empty((C, D), BF16, dev)
+        mean = _empty((C,), F32, dev)
+        rstd = _empty((C,), F32, dev)
+        ops.layernorm_fwd(x, c.ln_final.weight, c.ln_final.bias, lnf, mean, rstd, row_idx=eot)
+        f = _empty((C, self.projT.shape[0]), F32, dev)
+        ops.gemm_nt(lnf, self.projT, EPI_F32, f)
+        ctx = dict(saved=saved, x=x, eot=eot, mean=mean, rstd=rstd, C=C, L=L) if save else None
+        return f, ctx
+
+    def backward(self, ctx, df, grads):
+        c = self.clip
+        dev = df.device
+        C, L = ctx["C"], ctx["L"]
+        D = c.transformer.width
+        dfb = _empty(df.shape, BF16, dev)
+        ops.cast_bf16(df.contiguous(), dfb)
+        dln = _empty((C, D), F32, dev)
+        ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
+        dx = torch.zeros((C * L, D), dtype=F32, device=dev)
+        dxb = torch.zeros((C * L, D), dtype=BF16, device=dev)
+        ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
+                          row_idx=ctx["eot"])
+        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L)

@@ -1,0 +1,189 @@
+"""Tensor-level wrappers over the C ABI (include/lc_clip.h). Shape/stride checks happen here and
+again in the library; every call launches on torch's current stream of the tensor's device."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, ptr, stream_of
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32 = range(6)
+
+
+def _rowmajor(t, dtype, name):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D row-major view, got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+
+
+def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
+    """out = epilogue(alpha * A @ B^T + bias); A [M,K] bf16, B [N,K] bf16."""
+    _rowmajor(A, BF16, "A")
+    _rowmajor(B, BF16, "B")
+    M, K = A.shape
+    N = B.shape[0]
+    if B.shape[1] != K or out0.shape[0] != M or out0.shape[1] != N:
+        raise ValueError(f"gemm_nt shapes A{tuple(A.shape)} B{tuple(B.shape)} out{tuple(out0.shape)}")
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("gemm_nt bias must be a contiguous f32 vector of length N")
+    call("lc_gemm_nt", stream_of(A), epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
+         ptr(bias), float(alpha), ptr(out0), out0.stride(0), ptr(out1),
+         out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0)
+    return out0
+
+
+def gemm_tn(A, B, C, alpha=1.0):
+    """C[N1,N2] += alpha * A[M,N1]^T @ B[M,N2] (C f32)."""
+    _rowmajor(A, BF16, "A")
+    _rowmajor(B, BF16, "B")
+    _rowmajor(C, F32, "C")
+    M, N1 = A.shape
+    N2 = B.shape[1]
+    if B.shape[0] != M or C.shape[0] != N1 or C.shape[1] != N2:
+        raise ValueError("gemm_tn shape mismatch")
+    call("lc_gemm_tn", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
+         float(alpha), ptr(C), C.stride(0))
+    return C
+
+
+def layernorm_fwd(x, weight, bias, y, mean=None, rstd=None, row_idx=None):
+    _rowmajor(x, F32, "x")
+    rows = y.shape[0]
+    D = x.shape[1]
+    call("lc_layernorm_fwd", stream_of(x), rows, D, ptr(x), x.stride(0), ptr(row_idx),
+         ptr(weight), ptr(bias), ptr(y), 1 if y.dtype == F32 else 0, y.stride(0), ptr(mean),
+         ptr(rstd))
+    return y
+
+
+def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_idx=None):
+    rows = dy.shape[0]
+    D = x.shape[1]
+    call("lc_layernorm_bwd", stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+         dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
+         ptr(dx_bf16), dx.stride(0), ptr(row_idx))
+    return dx
+
+
+def patchify(img, patch, out):
+    if img.dtype != F32 or not img.is_contiguous():
+        raise ValueError("patchify expects a contiguous f32 NCHW batch")
+    n, c, h, w = img.shape
+    if c != 3 or h != w:
+        raise ValueError("patchify expects square 3-channel images")
+    call("lc_patchify", stream_of(img), n, h, patch, ptr(img), ptr(out))
+    return out
+
+
+def vit_assemble(patch_emb, cls, pos, x, n_img, n_patch):
+    call("lc_vit_assemble", stream_of(x), n_img, n_patch, x.shape[1], ptr(patch_emb), ptr(cls),
+         ptr(pos), ptr(x))
+    return x
+
+
+def text_embed(tokens, emb, pos, x):
+    if tokens.dtype != torch.int64 or not tokens.is_contiguous():
+        raise ValueError("tokens must be contiguous int64")
+    C, L = tokens.shape
+    call("lc_text_embed", stream_of(x), C, L, x.shape[1], ptr(tokens), ptr(emb), ptr(pos), ptr(x))
+    return x
+
+
+def eot_rows(tokens, out):
+    C, L = tokens.shape
+    call("lc_eot_rows", stream_of(tokens), C, L, ptr(tokens), ptr(out))
+    return out
+
+
+def attn_fwd(qkv, O, lse, n_seq, L, H, causal):
+    call("lc_attn_fwd", stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), O.stride(0),
+         ptr(lse), int(causal))
+    return O
+
+
+def attn_bwd(qkv, O, dO, lse, dqkv, n_seq, L, H, causal):
+    if O.stride(0) != dO.stride(0):
+        raise ValueError("O and dO must share a row stride")
+    call("lc_attn_bwd", stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), ptr(dO),
+         O.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), int(causal))
+    return dqkv
+
+
+def cast_bf16(src, dst):
+    if src.dtype != F32 or not src.is_contiguous() or not dst.is_contiguous():
+        raise ValueError("cast_bf16 expects contiguous f32 -> bf16")
+    call("lc_cast_bf16", stream_of(src), src.numel(), ptr(src), ptr(dst))
+    return dst
+
+
+def merge_weight(W, A, B, scaling, out, outT=None):
+    """out = bf16(W + scaling * B @ A); A/B None -> plain cast."""
+    N, K = W.shape
+    r = 0 if A is None else A.shape[0]
+    call("lc_merge_weight", stream_of(W), N, K, r, ptr(W), ptr(A), ptr(B), float(scaling),
+         ptr(out), ptr(outT))
+    return out
+
+
+def lora_grad(dY, X, A, B, scaling, dA, dB):
+    M, N = dY.shape
+    K = X.shape[1]
+    call("lc_lora_grad", stream_of(dY), M, N, K, A.shape[0], ptr(dY), dY.stride(0), ptr(X),
+         X.stride(0), ptr(A), ptr(B), float(scaling), ptr(dA), ptr(dB))
+
+
+def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h):
+    M, D = z.shape
+    call("lc_adapter_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
+         ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(resid), ptr(xout),
+         xout.stride(0), ptr(h))
+
+
+def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz, dbd, dbu):
+    M, D = gout.shape
+    call("lc_adapter_bwd", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
+         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz), dz.stride(0), ptr(dbd), ptr(dbu))
+
+
+def check_finite(g, flag):
+    call("lc_check_finite", stream_of(g), g.numel(), ptr(g), ptr(flag))
+
+
+def adamw(p, g, m, v, lr, b1, b2, eps, wd, step, skip=None):
+    call("lc_adamw", stream_of(p), p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), float(lr), float(b1),
+         float(b2), float(eps), float(wd), int(step), ptr(skip))
+
+
+def l2norm_rows(f, out, norms):
+    R, E = f.shape
+    call("lc_l2norm_rows", stream_of(f), R, E, ptr(f), f.stride(0), ptr(out), ptr(norms))
+
+
+def clip_head(img_n, txt_n, logit_scale, labels, probs, dlogits, loss):
+    B, E = img_n.shape
+    C = txt_n.shape[0]
+    call("lc_clip_head", stream_of(img_n), B, C, E, ptr(img_n), ptr(txt_n), ptr(logit_scale),
+         ptr(labels), ptr(probs), ptr(dlogits), ptr(loss))
+
+
+def head_logits(img_n, txt_n, logit_scale, logits, probs=None):
+    B, E = img_n.shape
+    C = txt_n.shape[0]
+    call("lc_head_logits", stream_of(img_n), B, C, E, ptr(img_n), ptr(txt_n), ptr(logit_scale),
+         ptr(logits), ptr(probs))
+
+
+def softmax_bwd_rows(probs, dprobs, dlogits):
+    B, C = probs.shape
+    call("lc_softmax_bwd_rows", stream_of(probs), B, C, ptr(probs), ptr(dprobs), ptr(dlogits))
+
+
+def head_feat_grad(dlogits, sr, sc, other_n, self_n, norms, logit_scale, dF, dn_ext=None):
+    R, E = self_n.shape
+    Co = other_n.shape[0]
+    call("lc_head_feat_grad", stream_of(dlogits), R, Co, E, ptr(dlogits), sr, sc, ptr(other_n),
+         ptr(self_n), ptr(norms), ptr(logit_scale), ptr(dn_ext), ptr(dF))

@@ -1,0 +1,445 @@
+"""CPU oracle for the CLIP dual-encoder PEFT training step — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product. Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it. The shipped path
+(``lifelong-clip_amd/lcclip``) never imports anything under ``oracle/`` and fails loudly
+when its HIP library is missing.
+
+What it restates (reference = qcNPU/LifeLong-CLIP @ 2024-12-18; citations are
+``path:line`` into that tree, which is read as text only — importing or running it was
+refused by the environment, see SURVEY.md §8(c) and DESIGN.md §Oracle):
+
+  * ``layer_norm``            models/clip/model.py:194-200   (fp32 upcast, eps 1e-5)
+  * ``quick_gelu``            models/clip/model.py:203-206   (x * sigmoid(1.702 x))
+  * ``mha``                   models/clip/lora.py:832-1074   (LoRA in-proj: shared A,
+                              stacked B, scaling alpha/r; q *= d_h^-0.5; bmm/softmax/bmm;
+                              out-proj + LoRA) and torch nn.MultiheadAttention for the
+                              vanilla/adapter blocks (model.py:217, 226-231)
+  * ``adapter``               models/clip/adapter.py:53-72   (down 64, ReLU, dropout,
+                              up, *scale, + residual; layernorm option 'none')
+  * ``block``                 models/clip/model.py:233-236 (vanilla / LoRA) and :439-442
+                              (adapter: the SAME adapter applied to both sub-blocks)
+  * ``encode_image``          models/clip/model.py:755-787   (Q1: ``blk(x)``, fixing :780)
+  * ``encode_text``           models/clip/model.py:941-956 + mask :926-932
+  * ``clip_logits``           models/clip/model.py:958-975
+  * ``adapter_clip_forward``  models/adapter_clip.py:94-100  (returns softmax probs)
+  * ``loss_on_probs``         methods/adapter_clip.py:88-89 + methods/_trainer.py:164
+                              (CrossEntropyLoss applied to the probabilities — Q5)
+  * ``adamw_step``            utils/train_utils.py:27-28 (torch.optim.AdamW, wd 1e-5)
+
+Parity pinning. The reference ships no tests, fixtures or golden vectors and could not be
+executed here, so the numeric restatement is pinned by the
+reference's own known answers and structural identities (tests/test_oracle.py):
+ViT-L/14 adapter-CLIP total/trainable parameter counts from nohup.out:8,29; the
+adapter-at-init == vanilla identity (adapter.py:49-51); out-proj LoRA B = 0 at init
+(lora.py:133-139); the vanilla block == torch's own nn.MultiheadAttention composition; and
+the double-softmax loss band. Golden fixtures under tests/golden/ are generated from this
+module by tests/golden/make_golden.py.
+
+Rounding hook. Every function takes ``rt`` (default identity). With ``rt = round_bf16`` the
+oracle rounds exactly where the MI355X path rounds (GEMM/attention operands and the bf16
+activations it stores), so the HIP forward can be checked at a tight tolerance; with the
+identity it is the plain fp32 reference algorithm.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+EOT_TOKEN = 49407
+SOT_TOKEN = 49406
+
+
+def identity(x):
+    return x
+
+
+def round_bf16(x):
+    """Round-to-nearest-even fp32 -> bf16 -> fp32 (value-preserving forward, STE backward)."""
+    r = x.detach().to(torch.bfloat16).to(x.dtype)
+    return x + (r - x).detach()
+
+
+@dataclass(frozen=True)
+class ClipConfig:
+    """CLIP shape parameters, inferred the way build_model does (model.py:1005-1049)."""
+    embed_dim: int = 512
+    image_resolution: int = 224
+    vision_layers: int = 12
+    vision_width: int = 768
+    vision_patch_size: int = 16
+    context_length: int = 77
+    vocab_size: int = 49408
+    transformer_width: int = 512
+    transformer_heads: int = 8
+    transformer_layers: int = 12
+
+    @property
+    def vision_heads(self):  # model.py:820
+        return self.vision_width // 64
+
+    @property
+    def grid(self):
+        return self.image_resolution // self.vision_patch_size
+
+
+VIT_B16 = ClipConfig()
+VIT_L14 = ClipConfig(embed_dim=768, vision_layers=24, vision_width=1024, vision_patch_size=14,
+                     transformer_width=768, transformer_heads=12)
+
+
+def tower_prefixes(cfg: ClipConfig):
+    vis = [f"visual.transformer.resblocks.{i}." for i in range(cfg.vision_layers)]
+    txt = [f"transformer.resblocks.{i}." for i in range(cfg.transformer_layers)]
+    return vis, txt
+
+
+def peft_on(peft_encoder: str, modal: str) -> bool:
+    """model.py:653-654: PEFT blocks are used when peft_encoder in ['both', modal]."""
+    return peft_encoder in ("both", modal)
+
+
+# ----------------------------------------------------------------------------- parameters
+def param_shapes(cfg: ClipConfig, method: str = "vanilla", peft_encoder: str = "none",
+                 lora_r: int = 4, ffn_num: int = 64):
+    """Name -> shape, in the reference's named_parameters() naming.
+
+    Backbone: model.py:709-729 (visual), 830-845 (text), 209-223 (blocks).
+    LoRA: lora.py:419-422 (in_proj_weight_lora_A [r, D], _B [3D, r]), lora.py:123-125
+    (out_proj.lora_A [r, D], lora_B [D, r]). Adapter: adapter.py:38-40 (down width is the
+    hard-coded 64, Q7). Block placement: model.py:652-683.
+    """
+    s = {}
+    W, P, E = cfg.vision_width, cfg.vision_patch_size, cfg.embed_dim
+    s["visual.class_embedding"] = (W,)
+    s["visual.positional_embedding"] = (cfg.grid ** 2 + 1, W)
+    s["visual.proj"] = (W, E)
+    s["visual.conv1.weight"] = (W, 3, P, P)
+    s["visual.ln_pre.weight"] = (W,)
+    s["visual.ln_pre.bias"] = (W,)
+    s["visual.ln_post.weight"] = (W,)
+    s["visual.ln_post.bias"] = (W,)
+    T = cfg.transformer_width
+    s["positional_embedding"] = (cfg.context_length, T)
+    s["text_projection"] = (T, E)
+    s["logit_scale"] = ()
+    s["token_embedding.weight"] = (cfg.vocab_size, T)
+    s["ln_final.weight"] = (T,)
+    s["ln_final.bias"] = (T,)
+    vis, txt = tower_prefixes(cfg)
+    for modal, width, prefixes in (("image", W, vis), ("text", T, txt)):
+        use = peft_on(peft_encoder, modal)
+        for pre in prefixes:
+            s[pre + "attn.in_proj_weight"] = (3 * width, width)
+            s[pre + "attn.in_proj_bias"] = (3 * width,)
+            if use and method == "lora":
+                s[pre + "attn.in_proj_weight_lora_A"] = (lora_r, width)
+                s[pre + "attn.in_proj_weight_lora_B"] = (3 * width, lora_r)
+            s[pre + "attn.out_proj.weight"] = (width, width)
+            s[pre + "attn.out_proj.bias"] = (width,)
+            if use and method == "lora":
+                s[pre + "attn.out_proj.lora_A"] = (lora_r, width)
+                s[pre + "attn.out_proj.lora_B"] = (width, lora_r)
+            s[pre + "ln_1.weight"] = (width,)
+            s[pre + "ln_1.bias"] = (width,)
+            s[pre + "mlp.c_fc.weight"] = (4 * width, width)
+            s[pre + "mlp.c_fc.bias"] = (4 * width,)
+            s[pre + "mlp.c_proj.weight"] = (width, 4 * width)
+            s[pre + "mlp.c_proj.bias"] = (width,)
+            s[pre + "ln_2.weight"] = (width,)
+            s[pre + "ln_2.bias"] = (width,)
+            if use and method == "adapter":
+                s[pre + "adaptmlp.down_proj.weight"] = (64, width)
+                s[pre + "adaptmlp.down_proj.bias"] = (64,)
+                s[pre + "adaptmlp.up_proj.weight"] = (width, ffn_num)
+                s[pre + "adaptmlp.up_proj.bias"] = (width,)
+    return s
+
+
+def is_trainable(name: str) -> bool:
+    """Freeze filter, methods/adapter_clip.py:117-119 (Q13)."""
+    return "adaptmlp" in name or "lora" in name
+
+
+# ----------------------------------------------------------------------------- primitives
+def layer_norm(x, w, b, eps=1e-5):
+    """model.py:194-200 — LayerNorm evaluated in fp32."""
+    return F.layer_norm(x.float(), (x.shape[-1],), w, b, eps)
+
+
+def quick_gelu(x):
+    """model.py:203-206."""
+    return x * torch.sigmoid(1.702 * x)
+
+
+def linear(x, w, b=None, rt=identity):
+    """F.linear with operands rounded at the GEMM input (fp32 accumulate)."""
+    y = rt(x) @ rt(w).t()
+    return y if b is None else y + b
+
+
+def merged_lora_weight(w, a, bmat, scaling, rt=identity):
+    """W + scaling * B @ A, rounded once: the MI355X path merges the rank-r update into the
+    frozen weight before the GEMM. Algebraically identical to lora.py:837-839 / 1072-1074
+    (F.linear(x, W) + F.linear(F.linear(x, A), B) * scaling)."""
+    return rt(w + scaling * (bmat @ a))
+
+
+def attention_core(q, k, v, scale, causal, rt=identity):
+    """lora.py:950 (q * scaling), 1043 (bmm), 1047-1051 (additive -inf mask), 1063 (softmax),
+    1068 (bmm). q,k,v: [N, H, L, dh]. With rt=round_bf16 it mirrors the HIP kernel: S in fp32
+    from bf16 q,k; P = exp(S - max) rounded to bf16 for the PV product; the row sum l is taken
+    from the unrounded fp32 exponentials; O = (P_bf16 @ V) / l, rounded to bf16."""
+    q, k, v = rt(q), rt(k), rt(v)
+    s = (q @ k.transpose(-1, -2)) * scale
+    if causal:
+        L = s.shape[-1]
+        mask = torch.full((L, L), float("-inf")).triu_(1)  # model.py:926-932
+        s = s + mask
+    m = s.amax(dim=-1, keepdim=True)
+    p = torch.exp(s - m)
+    l = p.sum(dim=-1, keepdim=True)
+    o = (rt(p) @ v) / l
+    return rt(o)
+
+
+def mha(x, p, pre, n_head, causal, lora_scaling=None, rt=identity):
+    """Self-attention for x [N, L, D] (batch-first internally; the reference's sequence-first
+    layout, model.py:767, is not observable). LoRA variant when the *_lora_* params exist:
+    qkv = F.linear(x, W, b) + F.linear(F.linear(x, A), B) * scaling (lora.py:837-839),
+    out = F.linear(o, Wo, bo) + F.linear(F.linear(o, Ao), Bo) * scaling (lora.py:1072-1074).
+    Returns the attention output BEFORE any rounding of the out-projection result."""
+    N, L, D = x.shape
+    dh = D // n_head
+    w_in = p[pre + "attn.in_proj_weight"]
+    w_out = p[pre + "attn.out_proj.weight"]
+    lora = (pre + "attn.in_proj_weight_lora_A") in p
+    if lora:
+        w_in = merged_lora_weight(w_in, p[pre + "attn.in_proj_weight_lora_A"],
+                                  p[pre + "attn.in_proj_weight_lora_B"], lora_scaling, rt)
+        w_out = merged_lora_weight(w_out, p[pre + "attn.out_proj.lora_A"],
+                                   p[pre + "attn.out_proj.lora_B"], lora_scaling, rt)
+    qkv = rt(linear(x, w_in, p[pre + "attn.in_proj_bias"], rt))
+    q, k, v = qkv.chunk(3, dim=-1)                                   # lora.py:840
+
+    def heads(t):                                                     # lora.py:1002-1006
+        return t.reshape(N, L, n_head, dh).permute(0, 2, 1, 3)
+    o = attention_core(heads(q), heads(k), heads(v), dh ** -0.5, causal, rt)
+    o = o.permute(0, 2, 1, 3).reshape(N, L, D)                        # lora.py:1070-1071
+    return linear(o, w_out, p[pre + "attn.out_proj.bias"], rt)
+
+
+def adapter(z, p, pre, scale=0.1, dropout_mask=None, rt=identity):
+    """adapter.py:53-72 with adapter_layernorm_option='none' (model.py:436):
+    out = z + scale * up(dropout(relu(down(z)))). ``dropout_mask`` (already divided by keep
+    probability) replaces F.dropout when given; None means eval / p = 0."""
+    d = torch.relu(linear(z, p[pre + "adaptmlp.down_proj.weight"],
+                          p[pre + "adaptmlp.down_proj.bias"], rt))
+    if dropout_mask is not None:
+        d = d * dropout_mask
+    u = linear(d, p[pre + "adaptmlp.up_proj.weight"], p[pre + "adaptmlp.up_proj.bias"], rt)
+    return z + scale * u
+
+
+def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, masks=None):
+    """ResidualAttentionBlock{,_LoRA} forward (model.py:233-236) and _Adapter forward
+    (model.py:439-442; one adapter module reused for both sub-blocks, Q6). x is the fp32
+    residual stream [N, L, D]."""
+    h = rt(layer_norm(x, p[pre + "ln_1.weight"], p[pre + "ln_1.bias"]))
+    a = mha(h, p, pre, n_head, causal, lora_scaling if variant == "lora" else None, rt)
+    if variant == "adapter":
+        m0 = None if masks is None else masks[0]
+        x = x + adapter(rt(a), p, pre, dropout_mask=m0, rt=rt)
+    else:
+        x = x + a
+    h2 = rt(layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"]))
+    f = rt(quick_gelu(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt)))
+    m = linear(f, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"], rt)
+    if variant == "adapter":
+        m1 = None if masks is None else masks[1]
+        x = x + adapter(rt(m), p, pre, dropout_mask=m1, rt=rt)
+    else:
+        x = x + m
+    return x
+
+
+def tower_variant(method: str, peft_encoder: str, modal: str) -> str:
+    if peft_on(peft_encoder, modal) and method in ("lora", "adapter"):
+        return method
+    return "vanilla"
+
+
+def encode_image(img, p, cfg: ClipConfig, method="vanilla", peft_encoder="none", rt=identity,
+                 masks=None):
+    """VisualTransformer.forward, model.py:755-787 (Q1: blocks called as blk(x))."""
+    N = img.shape[0]
+    W, P = cfg.vision_width, cfg.vision_patch_size
+    g = cfg.grid
+    # conv1 (k = s = P, no bias) == GEMM over [3*P*P] patches in (c, kh, kw) order
+    patches = img.reshape(N, 3, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(N, g * g, 3 * P * P)
+    x = linear(patches, p["visual.conv1.weight"].reshape(W, -1), None, rt)      # :756-758
+    cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
+    x = torch.cat([cls, x], dim=1)                                              # :759-763
+    x = x + p["visual.positional_embedding"]                                    # :764
+    x = layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])      # :766
+    variant = tower_variant(method, peft_encoder, "image")
+    vis, _ = tower_prefixes(cfg)
+    for i, pre in enumerate(vis):
+        x = block(x, p, pre, cfg.vision_heads, False, variant, rt=rt,
+                  masks=None if masks is None else masks[i])
+    x = rt(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))  # :783
+    return linear(x, p["visual.proj"].t(), None, rt)                            # :785
+
+
+def encode_text(tokens, p, cfg: ClipConfig, method="vanilla", peft_encoder="none", rt=identity,
+                masks=None):
+    """CLIP.encode_text, model.py:941-956; causal mask model.py:926-932; EOT pooling by
+    argmax of the token ids (Q11). ln_final is row-local, so gathering the EOT row first and
+    normalising it equals normalising all rows then gathering."""
+    C = tokens.shape[0]
+    x = p["token_embedding.weight"][tokens] + p["positional_embedding"]
+    variant = tower_variant(method, peft_encoder, "text")
+    _, txt = tower_prefixes(cfg)
+    for i, pre in enumerate(txt):
+        x = block(x, p, pre, cfg.transformer_heads, True, variant, rt=rt,
+                  masks=None if masks is None else masks[i])
+    eot = tokens.argmax(dim=-1)
+    x = x[torch.arange(C), eot]
+    x = rt(layer_norm(x, p["ln_final.weight"], p["ln_final.bias"]))
+    return linear(x, p["text_projection"].t(), None, rt)
+
+
+def clip_logits(img_f, txt_f, logit_scale):
+    """model.py:966-974: L2-normalise, logits = exp(logit_scale) * I @ T^T."""
+    i = img_f / img_f.norm(dim=-1, keepdim=True)
+    t = txt_f / txt_f.norm(dim=-1, keepdim=True)
+    return logit_scale.exp() * i @ t.t(), i, t
+
+
+def adapter_clip_forward(img, tokens, p, cfg, method, peft_encoder, rt=identity,
+                         img_masks=None, txt_masks=None):
+    """AdapterCLIP.forward, models/adapter_clip.py:94-100 -> (probs, img_f, txt_f)."""
+    fi = encode_image(img, p, cfg, method, peft_encoder, rt, img_masks)
+    ft = encode_text(tokens, p, cfg, method, peft_encoder, rt, txt_masks)
+    logits, i, t = clip_logits(fi, ft, p["logit_scale"])
+    return logits.softmax(dim=-1), i, t
+
+
+def loss_on_probs(probs, y):
+    """nn.CrossEntropyLoss()(probs, y) — applied to probabilities (Q5)."""
+    return F.cross_entropy(probs, y)
+
+
+def adamw_step(params, grads, state, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, wd=1e-5):
+    """One torch.optim.AdamW step (utils/train_utils.py:27-28), written out so the semantics
+    are explicit. state: dict name -> (step, m, v)."""
+    b1, b2 = betas
+    out = {}
+    for n, prm in params.items():
+        g = grads[n]
+        step, m, v = state.get(n, (0, torch.zeros_like(prm), torch.zeros_like(prm)))
+        step += 1
+        prm = prm * (1 - lr * wd)
+        m = b1 * m + (1 - b1) * g
+        v = b2 * v + (1 - b2) * g * g
+        bc1 = 1 - b1 ** step
+        bc2 = 1 - b2 ** step
+        denom = (v / bc2).sqrt() + eps
+        prm = prm - (lr / bc1) * m / denom
+        state[n] = (step, m, v)
+        out[n] = prm
+    return out
+
+
+def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-4):
+    """methods/adapter_clip.py:86-96 at p=0 dropout: fwd -> CE(probs) -> bwd -> AdamW.
+    Returns (loss, probs, img_f, txt_f, grads, new_params)."""
+    leaves = {n: t.detach().clone().requires_grad_(is_trainable(n)) for n, t in p.items()}
+    probs, fi, ft = adapter_clip_forward(img, tokens, leaves, cfg, method, peft_encoder, rt)
+    loss = loss_on_probs(probs, y)
+    train = {n: t for n, t in leaves.items() if t.requires_grad}
+    if not train:  # vanilla blocks: nothing is trainable (the freeze filter leaves no params)
+        return loss.detach(), probs.detach(), fi.detach(), ft.detach(), {}, {}
+    grads = dict(zip(train.keys(), torch.autograd.grad(loss, list(train.values()))))
+    new = adamw_step({n: t.detach() for n, t in train.items()}, grads, {}, lr=lr)
+    return loss.detach(), probs.detach(), fi.detach(), ft.detach(), grads, new
+
+
+# ----------------------------------------------------------------------------- synthetic data
+def synthetic_images(n, res=224, seed=0):
+    """U[0,1) images normalised with the CIFAR-100 statistics
+    (datasets/__init__.py:38-39)."""
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(n, 3, res, res, generator=g)
+    mean = torch.tensor([0.5071, 0.4867, 0.4408]).view(1, 3, 1, 1)
+    std = torch.tensor([0.2675, 0.2565, 0.2761]).view(1, 3, 1, 1)
+    return (x - mean) / std
+
+
+def synthetic_tokens(c, context_length=77, seed=0, vocab=49408):
+    """C rows [SOT, t_1..t_k, EOT, 0...], k ~ U{6..12}, t ~ U{256..49405}.
+    SOT/EOT are the two highest ids (49406/49407 for the CLIP vocab), so EOT pooling by argmax
+    (model.py:953-954) finds the EOT position."""
+    g = torch.Generator().manual_seed(seed + 7)
+    sot, eot = vocab - 2, vocab - 1
+    lo = min(256, vocab // 4)
+    out = torch.zeros(c, context_length, dtype=torch.long)
+    for i in range(c):
+        k = int(torch.randint(6, 13, (1,), generator=g))
+        body = torch.randint(lo, sot, (k,), generator=g)
+        out[i, 0] = sot
+        out[i, 1:1 + k] = body
+        out[i, 1 + k] = eot
+    return out
+
+
+def synthetic_state_dict(cfg: ClipConfig, method="vanilla", peft_encoder="none", seed=1234,
+                         peft_nonzero=True):
+    """Seeded weights in the reference's state-dict layout with CLIP-like statistics
+    (model.py:852-885; Linear-style fan-in scaling elsewhere). With peft_nonzero the LoRA B and
+    adapter up weights are NONZERO so the PEFT forward and dW paths are exercised (SURVEY.md
+    §8(c): zero inits would hide bugs); biases are nonzero too."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for name, shape in param_shapes(cfg, method, peft_encoder).items():
+        if name == "logit_scale":
+            sd[name] = torch.tensor(math.log(1 / 0.07))
+            continue
+        if name.endswith("ln_1.weight") or name.endswith("ln_2.weight") or name.endswith(
+                ("ln_pre.weight", "ln_post.weight", "ln_final.weight")):
+            sd[name] = 1.0 + 0.1 * torch.randn(shape, generator=g)
+            continue
+        if name.endswith("bias") and "ln_" in name:
+            sd[name] = 0.05 * torch.randn(shape, generator=g)
+            continue
+        if name.endswith("bias"):
+            sd[name] = 0.02 * torch.randn(shape, generator=g)
+            continue
+        if "lora_B" in name or "up_proj.weight" in name:
+            std = 0.05 if peft_nonzero else 0.0
+            sd[name] = std * torch.randn(shape, generator=g)
+            continue
+        if name in ("token_embedding.weight",):
+            sd[name] = 0.02 * torch.randn(shape, generator=g)
+            continue
+        if name == "positional_embedding":
+            sd[name] = 0.01 * torch.randn(shape, generator=g)
+            continue
+        if len(shape) == 1:
+            sd[name] = (shape[0] ** -0.5) * torch.randn(shape, generator=g)
+            continue
+        fan_in = 1
+        for s in shape[1:]:
+            fan_in *= s
+        if name in ("visual.proj", "text_projection", "visual.positional_embedding"):
+            fan_in = shape[0]
+        sd[name] = (fan_in ** -0.5) * torch.randn(shape, generator=g)
+    return sd
+
+
+TINY = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=2, vision_width=128,
+                  vision_patch_size=16, context_length=77, vocab_size=512, transformer_width=64,
+                  transformer_heads=1, transformer_layers=2)

@@ -1,0 +1,160 @@
+"""CPU tests that pin the oracle (oracle/clip_oracle.py) to the reference's known answers and
+structural identities, and freeze it against the committed golden fixtures."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from oracle import clip_oracle as o
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "tiny_clip.npz")
+
+
+def count(cfg, method, peft):
+    shapes = o.param_shapes(cfg, method, peft)
+    total = sum(math.prod(s) for s in shapes.values())
+    train = sum(math.prod(s) for n, s in shapes.items() if o.is_trainable(n))
+    return total, train
+
+
+def test_vit_l14_adapter_param_counts_match_reference_log():
+    # nohup.out:8 "Total Parameters : 431977985"; nohup.out:29 "Trainable parameters: 4361472"
+    # (ViT-L/14 CLIP + adapter on both towers)
+    total, train = count(o.VIT_L14, "adapter", "both")
+    assert total == 431_977_985
+    assert train == 4_361_472
+
+
+def test_vit_b16_param_counts():
+    # ViT-B/16 CLIP 149 620 737; PEFT both towers LoRA 368 640, adapter 1 982 976
+    assert count(o.VIT_B16, "vanilla", "none")[0] == 149_620_737
+    assert count(o.VIT_B16, "lora", "both")[1] == 368_640
+    assert count(o.VIT_B16, "adapter", "both")[1] == 1_982_976
+
+
+def _tiny_inputs():
+    cfg = o.TINY
+    img = o.synthetic_images(2, cfg.image_resolution, seed=3)
+    tok = o.synthetic_tokens(3, cfg.context_length, seed=3, vocab=cfg.vocab_size)
+    return cfg, img, tok
+
+
+def test_adapter_at_init_equals_vanilla_bitwise():
+    # adapter.py:49-51: up.weight = up.bias = 0 -> the adapter block is the vanilla block exactly
+    cfg, img, tok = _tiny_inputs()
+    sd = o.synthetic_state_dict(cfg, "adapter", "both", seed=5, peft_nonzero=False)
+    for k in sd:
+        if "up_proj.bias" in k:
+            sd[k].zero_()
+    van = {k: v for k, v in sd.items() if "adaptmlp" not in k}
+    pa, ia, ta = o.adapter_clip_forward(img, tok, sd, cfg, "adapter", "both")
+    pv, iv, tv = o.adapter_clip_forward(img, tok, van, cfg, "vanilla", "none")
+    assert torch.equal(ia, iv) and torch.equal(ta, tv) and torch.equal(pa, pv)
+
+
+def test_lora_out_proj_zero_at_init_in_proj_not():
+    # lora.py:133-139 (out-proj B zeros) vs lora.py:451-452 (in-proj A, B xavier -> nonzero)
+    cfg, img, tok = _tiny_inputs()
+    sd = o.synthetic_state_dict(cfg, "lora", "both", seed=5, peft_nonzero=True)
+    for k in sd:
+        if k.endswith("out_proj.lora_B"):
+            sd[k].zero_()
+    van = {k: v for k, v in sd.items() if "lora" not in k}
+    _, i_l, _ = o.adapter_clip_forward(img, tok, sd, cfg, "lora", "both")
+    _, i_v, _ = o.adapter_clip_forward(img, tok, van, cfg, "vanilla", "none")
+    assert not torch.allclose(i_l, i_v)  # in-proj LoRA is live at init
+    sd2 = dict(sd)
+    for k in sd2:
+        if k.endswith("in_proj_weight_lora_B"):
+            sd2[k] = torch.zeros_like(sd2[k])
+    _, i_l0, _ = o.adapter_clip_forward(img, tok, sd2, cfg, "lora", "both")
+    torch.testing.assert_close(i_l0, i_v, rtol=1e-6, atol=1e-6)
+
+
+def test_vanilla_block_matches_torch_multihead_attention():
+    # model.py:217,226-236: the vanilla block is torch's nn.MultiheadAttention + LN + MLP
+    torch.manual_seed(0)
+    D, H, L, N = 128, 2, 17, 3
+    sd = {}
+    pre = "b."
+    mha = nn.MultiheadAttention(D, H)
+    sd[pre + "attn.in_proj_weight"] = mha.in_proj_weight.detach()
+    sd[pre + "attn.in_proj_bias"] = torch.randn(3 * D) * 0.1
+    sd[pre + "attn.out_proj.weight"] = mha.out_proj.weight.detach()
+    sd[pre + "attn.out_proj.bias"] = torch.randn(D) * 0.1
+    with torch.no_grad():
+        mha.in_proj_bias.copy_(sd[pre + "attn.in_proj_bias"])
+        mha.out_proj.bias.copy_(sd[pre + "attn.out_proj.bias"])
+    ln1, ln2 = nn.LayerNorm(D), nn.LayerNorm(D)
+    fc, pr = nn.Linear(D, 4 * D), nn.Linear(4 * D, D)
+    for name, mod in (("ln_1", ln1), ("ln_2", ln2), ("mlp.c_fc", fc), ("mlp.c_proj", pr)):
+        with torch.no_grad():
+            mod.weight.add_(0.1 * torch.randn_like(mod.weight))
+            mod.bias.add_(0.1 * torch.randn_like(mod.bias))
+        sd[pre + name + ".weight"] = mod.weight.detach()
+        sd[pre + name + ".bias"] = mod.bias.detach()
+    x = torch.randn(N, L, D)
+    for causal in (False, True):
+        mask = torch.full((L, L), float("-inf")).triu_(1) if causal else None
+        xs = x.permute(1, 0, 2)
+        with torch.no_grad():
+            a = mha(ln1(xs), ln1(xs), ln1(xs), need_weights=False, attn_mask=mask)[0]
+            y = xs + a
+            h = fc(ln2(y))
+            y = y + pr(h * torch.sigmoid(1.702 * h))
+        got = o.block(x, sd, pre, H, causal, "vanilla")
+        torch.testing.assert_close(got, y.permute(1, 0, 2), rtol=1e-5, atol=1e-5)
+
+
+def test_loss_band_double_softmax():
+    # CE(probs) in [log(C-1+e)-1, log(C-1+e)]
+    for C in (3, 10, 100):
+        probs = torch.softmax(torch.randn(64, C) * 5, dim=-1)
+        y = torch.randint(0, C, (64,))
+        loss = o.loss_on_probs(probs, y)
+        hi = math.log(C - 1 + math.e)
+        assert hi - 1 - 1e-6 <= loss.item() <= hi + 1e-6
+
+
+def test_adamw_matches_torch():
+    torch.manual_seed(0)
+    p = torch.randn(10)
+    g = torch.randn(10)
+    new = o.adamw_step({"p": p}, {"p": g}, {}, lr=5e-4)["p"]
+    q = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([q], lr=5e-4, weight_decay=1e-5)
+    q.grad = g.clone()
+    opt.step()
+    torch.testing.assert_close(new, q.detach(), rtol=0, atol=1e-7)
+
+
+def test_bf16_rounding_mode_is_close_to_fp32():
+    cfg, img, tok = _tiny_inputs()
+    sd = o.synthetic_state_dict(cfg, "adapter", "both", seed=9)
+    p32, i32, t32 = o.adapter_clip_forward(img, tok, sd, cfg, "adapter", "both")
+    p16, i16, t16 = o.adapter_clip_forward(img, tok, sd, cfg, "adapter", "both", rt=o.round_bf16)
+    assert (p32 - p16).abs().max() < 2e-2
+    assert not torch.equal(i32, i16)
+
+
+@pytest.mark.parametrize("method", ["vanilla", "lora", "adapter"])
+def test_oracle_reproduces_golden(method):
+    d = np.load(GOLDEN)
+    cfg = o.TINY
+    names = o.param_shapes(cfg, method, "both").keys()
+    p = {k: torch.from_numpy(d["sd/" + k]) for k in names}
+    img, tok, y = (torch.from_numpy(d[k]) for k in ("images", "tokens", "labels"))
+    loss, probs, fi, ft, grads, new = o.train_step(img, tok, y, p, cfg, method, "both")
+    np.testing.assert_allclose(probs.numpy(), d[f"{method}/probs"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(fi.numpy(), d[f"{method}/img_f"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(ft.numpy(), d[f"{method}/txt_f"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(loss.reshape(1).numpy(), d[f"{method}/loss"], rtol=1e-6)
+    for k, g in grads.items():
+        np.testing.assert_allclose(g.numpy(), d[f"{method}/grad/{k}"], rtol=1e-4, atol=1e-7)
+        np.testing.assert_allclose(new[k].numpy(), d[f"{method}/new/{k}"], rtol=1e-6, atol=1e-8)
+    # loss band (C = 3)
+    hi = math.log(2 + math.e)
+    assert hi - 1 <= loss.item() <= hi
