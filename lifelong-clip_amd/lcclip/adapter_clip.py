@@ -44,6 +44,27 @@ class AdapterCLIP(nn.Module):
         self.prompt_template = "a bad photo of a {}."
         self._tokenizer = tokenizer
 
+    @classmethod
+    def from_state_dict(cls, state_dict, peft_method="adapter", peft_encoder="both", device=None,
+                        tokenizer=None):
+        """Build from an in-memory CLIP state dict (the path clip_loader.load takes for a local
+        checkpoint file, clip_loader.py:116-135)."""
+        from .model import build_model
+        self = cls.__new__(cls)
+        nn.Module.__init__(self)
+        self.device = device
+        dd = {"method": peft_method, "peft_encoder": peft_encoder, "ffn_num": 64, "lora_alpha": 1,
+              "lora_r": 4}
+        self.model = build_model(dict(state_dict), dd)
+        if device is not None:
+            self.model = self.model.to(device)
+        self.text_tokens = None
+        self.current_class_names = []
+        self.dtype = self.model.dtype
+        self.prompt_template = "a bad photo of a {}."
+        self._tokenizer = tokenizer
+        return self
+
     @property
     def module(self):
         return self
@@ -102,6 +123,15 @@ class AdapterCLIP(nn.Module):
         elif hasattr(self, "text_tokens"):
             del self.text_tokens
         self.register_buffer("text_tokens", tokens)
+
+
+def set_adapter_dropout(model: nn.Module, p: float):
+    """Set the adapter dropout probability (adapter.py:61; 0.1 in the reference). Parity tests use
+    p = 0 because a dropout RNG stream cannot be matched bit-exactly."""
+    for m in model.modules():
+        if m.__class__.__name__ == "Adapter":
+            m.dropout = float(p)
+    return model
 
 
 def freeze_backbone(model: nn.Module):

@@ -1,0 +1,322 @@
+"""Per-kernel parity on the MI355X: every HIP kernel vs a plain torch fp32 reference of the same op
+evaluated on the same bf16-rounded inputs. Tolerances are stated per test: bf16 OUTPUTS carry a
+rounding of 2^-9 relative, so bf16-output checks use a relative-norm bound of 4e-3 (fp32 outputs
+1e-4); exact-integer tests catch layout bugs bit-exactly."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from lcclip import ops as _ops
+    return _ops
+
+
+# ------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(300, 128, 64), (1000, 384, 768), (77, 192, 128),
+                                   (4096, 768, 3072), (33, 64, 512)])
+def test_gemm_nt_exact_integers(ops, dev, M, N, K):
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device=dev, generator=g).to(BF)
+    B = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(BF)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_nt(A, B, ops.EPI_F32, out)
+    ref = A.float() @ B.float().t()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 384, 768), (77, 192, 128), (197 * 3, 2304, 768)])
+def test_gemm_nt_epilogues(ops, dev, M, N, K):
+    torch.manual_seed(0)
+    A = torch.randn(M, K, device=dev).to(BF)
+    B = (torch.randn(N, K, device=dev) * K ** -0.5).to(BF)
+    bias = torch.randn(N, device=dev)
+    ref = A.float() @ B.float().t() + bias
+    o = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_BF16, o, bias=bias)
+    assert rel(o, ref) < 4e-3
+    o32 = torch.empty(M, N, device=dev)
+    ops.gemm_nt(A, B, ops.EPI_F32, o32, bias=bias, alpha=1.0)
+    assert rel(o32, ref) < 1e-5
+    res = torch.randn(M, N, device=dev)
+    ops.gemm_nt(A, B, ops.EPI_RESID, o32, bias=bias, aux=res)
+    assert rel(o32, ref + res) < 1e-5
+    pre = torch.empty(M, N, device=dev, dtype=BF)
+    gl = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_GELU, pre, bias=bias, out1=gl)
+    assert rel(pre, ref) < 4e-3
+    assert rel(gl, ref * torch.sigmoid(1.702 * ref)) < 4e-3
+    # GELU backward epilogue: out = (alpha * A B^T) * qgelu'(aux)
+    aux = torch.randn(M, N, device=dev).to(BF)
+    a = aux.float()
+    s = torch.sigmoid(1.702 * a)
+    dg = s + 1.702 * a * s * (1 - s)
+    ob = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_GELU_BWD, ob, alpha=0.5, aux=aux)
+    assert rel(ob, 0.5 * (A.float() @ B.float().t()) * dg) < 4e-3
+    # strided A view (row stride > K)
+    Aw = torch.randn(M, K + 64, device=dev).to(BF)[:, 64:]
+    ops.gemm_nt(Aw, B, ops.EPI_F32, o32)
+    assert rel(o32, Aw.float() @ B.float().t()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N1,N2", [(100, 128, 64), (3000, 64, 768), (50432 // 8, 768, 64)])
+def test_gemm_tn(ops, dev, M, N1, N2):
+    torch.manual_seed(1)
+    A = torch.randn(M, N1, device=dev).to(BF)
+    B = torch.randn(M, N2, device=dev).to(BF)
+    C = torch.ones(N1, N2, device=dev)
+    ops.gemm_tn(A, B, C, alpha=0.5)
+    ref = 1 + 0.5 * A.float().t() @ B.float()
+    assert rel(C - 1, ref - 1) < 1e-5
+
+
+# ------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [64, 128, 512, 768])
+def test_layernorm_fwd_bwd(ops, dev, D):
+    torch.manual_seed(2)
+    R = 333
+    x = torch.randn(R, D, device=dev) * 3 + 1
+    w = torch.randn(D, device=dev)
+    b = torch.randn(D, device=dev)
+    y = torch.empty(R, D, device=dev, dtype=BF)
+    mean = torch.empty(R, device=dev)
+    rstd = torch.empty(R, device=dev)
+    ops.layernorm_fwd(x, w, b, y, mean, rstd)
+    xr = x.clone().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xr, (D,), w, b, 1e-5)
+    assert rel(y, ref) < 4e-3
+    y32 = torch.empty(R, D, device=dev)
+    ops.layernorm_fwd(x, w, b, y32)
+    assert rel(y32, ref) < 1e-5
+    dy = torch.randn(R, D, device=dev).to(BF)
+    ref.backward(dy.float())
+    dres = torch.randn(R, D, device=dev)
+    dx = torch.empty(R, D, device=dev)
+    dxb = torch.empty(R, D, device=dev, dtype=BF)
+    ops.layernorm_bwd(dy, x, mean, rstd, w, dx, dxb, dres=dres)
+    assert rel(dx, xr.grad + dres) < 1e-4
+    assert rel(dxb, xr.grad + dres) < 4e-3
+    # gathered rows (ln_post on CLS rows / ln_final on EOT rows)
+    idx = torch.tensor([0, 17, 34, 200], device=dev, dtype=torch.int32)
+    yg = torch.empty(4, D, device=dev)
+    mg = torch.empty(4, device=dev)
+    rg = torch.empty(4, device=dev)
+    ops.layernorm_fwd(x, w, b, yg, mg, rg, row_idx=idx)
+    assert rel(yg, ref.detach()[idx.long()]) < 1e-5
+    dyg = torch.randn(4, D, device=dev)
+    dxg = torch.zeros(R, D, device=dev)
+    ops.layernorm_bwd(dyg, x, mg, rg, w, dxg, None, row_idx=idx)
+    xr2 = x[idx.long()].clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr2, (D,), w, b, 1e-5).backward(dyg)
+    assert rel(dxg[idx.long()], xr2.grad) < 1e-4
+    assert dxg.abs().sum() == dxg[idx.long()].abs().sum()
+
+
+# ------------------------------------------------------------------------------- attention
+def ref_attention(q, k, v, causal):
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if causal:
+        L = s.shape[-1]
+        s = s + torch.full((L, L), float("-inf"), device=s.device).triu_(1)
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("n,L,H,causal", [(3, 17, 2, False), (4, 77, 8, True), (2, 197, 12, False),
+                                          (5, 32, 1, True), (2, 200, 2, False), (3, 224, 2, False)])
+def test_attention_fwd_bwd(ops, dev, n, L, H, causal):
+    torch.manual_seed(3)
+    D = H * 64
+    qkv = (torch.randn(n * L, 3 * D, device=dev) * 1.5).to(BF)
+    O = torch.empty(n * L, D, device=dev, dtype=BF)
+    lse = torch.empty(n * H, L, device=dev)
+    ops.attn_fwd(qkv, O, lse, n, L, H, causal)
+    t = qkv.float().reshape(n, L, 3, H, 64).permute(2, 0, 3, 1, 4)  # 3, n, H, L, 64
+    q, k, v = (x.clone().requires_grad_(True) for x in t)
+    ref = ref_attention(q, k, v, causal)
+    got = O.float().reshape(n, L, H, 64).permute(0, 2, 1, 3)
+    assert rel(got, ref) < 8e-3
+    s = (q @ k.transpose(-1, -2)) * 0.125
+    if causal:
+        s = s + torch.full((L, L), float("-inf"), device=dev).triu_(1)
+    ref_lse = torch.logsumexp(s, -1) / math.log(2)
+    assert rel(lse.reshape(n, H, L), ref_lse) < 1e-4
+    if L > 224:
+        return
+    dO = torch.randn(n * L, D, device=dev).to(BF)
+    dqkv = torch.empty(n * L, 3 * D, device=dev, dtype=BF)
+    ops.attn_bwd(qkv, O, dO, lse, dqkv, n, L, H, causal)
+    # reference gradient through the attention actually computed (its O is the bf16 one)
+    ref.backward(dO.float().reshape(n, L, H, 64).permute(0, 2, 1, 3))
+    g = dqkv.float().reshape(n, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    assert rel(g[0], q.grad) < 2e-2
+    assert rel(g[1], k.grad) < 2e-2
+    assert rel(g[2], v.grad) < 2e-2
+
+
+# ------------------------------------------------------------------------------- PEFT
+@pytest.mark.parametrize("D,M,keep", [(768, 1000, 1.0), (128, 77, 1.0), (512, 300, 0.9)])
+def test_adapter_fwd_bwd(ops, dev, D, M, keep):
+    torch.manual_seed(4)
+    z = torch.randn(M, D, device=dev).to(BF)
+    Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
+    bd = torch.randn(64, device=dev) * 0.1
+    Wu = (torch.randn(D, 64, device=dev) * 0.125).to(BF)
+    bu = torch.randn(D, device=dev) * 0.1
+    resid = torch.randn(M, D, device=dev)
+    x = torch.empty(M, D, device=dev)
+    h = torch.empty(M, 64, device=dev, dtype=BF)
+    ops.adapter_fwd(z, Wd, bd, Wu, bu, 0.1, keep, 1234, resid, x, h)
+    hr = torch.relu(z.float() @ Wd.float().t() + bd)
+    if keep < 1.0:
+        kept = h.float() > 0
+        assert (kept <= (hr > 0)).all()
+        frac = kept[hr > 0].float().mean().item()
+        assert abs(frac - keep) < 0.03  # dropout keep rate
+        hr = torch.where(kept, hr / keep, torch.zeros_like(hr))
+    assert rel(h, hr) < 4e-3
+    ref = resid + z.float() + 0.1 * (h.float() @ Wu.float().t() + bu)
+    assert rel(x, ref) < 1e-4
+    # backward
+    g = torch.randn(M, D, device=dev).to(BF)
+    dpre = torch.empty(M, 64, device=dev, dtype=BF)
+    dz = torch.empty(M, D, device=dev, dtype=BF)
+    dbd = torch.zeros(64, device=dev)
+    dbu = torch.zeros(D, device=dev)
+    ops.adapter_bwd(g, h, Wu.t().contiguous(), Wd.t().contiguous(), 0.1, keep, dpre, dz, dbd, dbu)
+    dh = 0.1 * g.float() @ Wu.float()
+    dpr = torch.where(h.float() > 0, dh / keep, torch.zeros_like(dh))
+    assert rel(dpre, dpr) < 4e-3
+    assert rel(dz, g.float() + dpre.float() @ Wd.float()) < 4e-3
+    assert rel(dbd, dpre.float().sum(0)) < 1e-4
+    assert rel(dbu, 0.1 * g.float().sum(0)) < 1e-4
+
+
+def test_lora_merge_and_grad(ops, dev):
+    torch.manual_seed(5)
+    N, K, r, M = 2304, 768, 4, 2000
+    W = torch.randn(N, K, device=dev)
+    A = torch.randn(r, K, device=dev)
+    B = torch.randn(N, r, device=dev)
+    out = torch.empty(N, K, device=dev, dtype=BF)
+    outT = torch.empty(K, N, device=dev, dtype=BF)
+    ops.merge_weight(W, A, B, 0.25, out, outT)
+    ref = W + 0.25 * B @ A
+    assert rel(out, ref) < 4e-3
+    assert torch.equal(outT, out.t())
+    dY = torch.randn(M, N, device=dev).to(BF)
+    X = torch.randn(M, K, device=dev).to(BF)
+    dA = torch.zeros(r, K, device=dev)
+    dB = torch.zeros(N, r, device=dev)
+    ops.lora_grad(dY, X, A, B, 0.25, dA, dB)
+    assert rel(dB, 0.25 * dY.float().t() @ (X.float() @ A.t())) < 1e-4
+    assert rel(dA, 0.25 * (dY.float() @ B).t() @ X.float()) < 1e-4
+
+
+def test_adamw_matches_torch(ops, dev):
+    torch.manual_seed(6)
+    n = 10007
+    p = torch.randn(n, device=dev)
+    q = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([q], lr=5e-4, weight_decay=1e-5)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    skip = torch.zeros(1, device=dev, dtype=torch.int32)
+    for step in range(1, 4):
+        g = torch.randn(n, device=dev)
+        q.grad = g.clone()
+        opt.step()
+        ops.check_finite(g, skip)
+        ops.adamw(p, g, m, v, 5e-4, 0.9, 0.999, 1e-8, 1e-5, step, skip)
+    assert rel(p, q.detach()) < 1e-6
+    g[5] = float("inf")
+    before = p.clone()
+    ops.check_finite(g, skip)
+    ops.adamw(p, g, m, v, 5e-4, 0.9, 0.999, 1e-8, 1e-5, 4, skip)
+    assert skip.item() == 1 and torch.equal(p, before)  # GradScaler-style skip
+
+
+# ------------------------------------------------------------------------------- embeddings
+def test_patchify_assemble_text_embed(ops, dev):
+    torch.manual_seed(7)
+    n, res, P, D = 3, 64, 16, 128
+    img = torch.randn(n, 3, res, res, device=dev)
+    g = res // P
+    patches = torch.empty(n * g * g, 3 * P * P, device=dev, dtype=BF)
+    ops.patchify(img, P, patches)
+    ref = img.reshape(n, 3, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(n * g * g, -1)
+    assert torch.equal(patches, ref.to(BF))
+    pe = torch.randn(n * g * g, D, device=dev)
+    cls = torch.randn(D, device=dev)
+    pos = torch.randn(g * g + 1, D, device=dev)
+    x = torch.empty(n * (g * g + 1), D, device=dev)
+    ops.vit_assemble(pe, cls, pos, x, n, g * g)
+    refx = torch.cat([cls.expand(n, 1, D), pe.reshape(n, g * g, D)], 1) + pos
+    assert torch.equal(x, refx.reshape(-1, D))
+    C, L, V = 5, 77, 512
+    tok = torch.randint(0, 500, (C, L), device=dev)
+    tok[torch.arange(C), torch.tensor([3, 9, 76, 0, 40])] = 511
+    emb = torch.randn(V, D, device=dev)
+    posT = torch.randn(L, D, device=dev)
+    xt = torch.empty(C * L, D, device=dev)
+    ops.text_embed(tok, emb, posT, xt)
+    assert torch.equal(xt, (emb[tok] + posT).reshape(-1, D))
+    eot = torch.empty(C, device=dev, dtype=torch.int32)
+    ops.eot_rows(tok, eot)
+    assert eot.tolist() == [c * L + t for c, t in enumerate(tok.argmax(-1).tolist())]
+
+
+# ------------------------------------------------------------------------------- head
+@pytest.mark.parametrize("B,C", [(2, 3), (256, 10), (64, 200)])
+def test_head_fused_and_module_kernels(ops, dev, B, C):
+    torch.manual_seed(8)
+    E = 512
+    fi = torch.randn(B, E, device=dev)
+    ft = torch.randn(C, E, device=dev)
+    ls = torch.tensor([math.log(1 / 0.07)], device=dev)
+    y = torch.randint(0, C, (B,), device=dev)
+    fir, ftr = fi.clone().requires_grad_(True), ft.clone().requires_grad_(True)
+    i_n = fir / fir.norm(dim=-1, keepdim=True)
+    t_n = ftr / ftr.norm(dim=-1, keepdim=True)
+    logits = ls.exp() * i_n @ t_n.t()
+    probs_ref = logits.softmax(-1)
+    loss_ref = torch.nn.functional.cross_entropy(probs_ref, y)
+    loss_ref.backward()
+    img_n = torch.empty_like(fi)
+    txt_n = torch.empty_like(ft)
+    ni = torch.empty(B, device=dev)
+    nt = torch.empty(C, device=dev)
+    ops.l2norm_rows(fi, img_n, ni)
+    ops.l2norm_rows(ft, txt_n, nt)
+    probs = torch.empty(B, C, device=dev)
+    dlog = torch.empty(B, C, device=dev)
+    loss = torch.zeros(1, device=dev)
+    ops.clip_head(img_n, txt_n, ls, y, probs, dlog, loss)
+    assert rel(probs, probs_ref) < 1e-5
+    assert abs(loss.item() - loss_ref.item()) < 1e-5
+    di = torch.empty_like(fi)
+    dt = torch.empty_like(ft)
+    ops.head_feat_grad(dlog, C, 1, txt_n, img_n, ni, ls, di)
+    ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, ls, dt)
+    assert rel(di, fir.grad) < 1e-4
+    assert rel(dt, ftr.grad) < 1e-4
+    # module-path kernels: logits/probs and softmax backward
+    lg = torch.empty(B, C, device=dev)
+    pr = torch.empty(B, C, device=dev)
+    ops.head_logits(img_n, txt_n, ls, lg, pr)
+    assert rel(lg, logits) < 1e-5 and rel(pr, probs_ref) < 1e-5
+    dp = torch.randn(B, C, device=dev)
+    dl = torch.empty(B, C, device=dev)
+    ops.softmax_bwd_rows(pr, dp, dl)
+    assert rel(dl, pr * (dp - (pr * dp).sum(-1, keepdim=True))) < 1e-5
