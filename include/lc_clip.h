@@ -46,11 +46,17 @@ int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, 
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux);
 
-/* C[N1,N2] += alpha * A[M,N1]^T . B[M,N2] (f32 C, atomically accumulated; split over M).
- * Replaces: the autograd weight-gradient GEMMs of adapter down_proj / up_proj
+/* Tile-shape override for lc_gemm_nt (tuning): 0 = automatic, 1 = 128x128 (4 waves),
+ * 2 = 256x128 (8 waves, 3-stage LDS ring), 3 = 256x256 (8 waves, 2 stages), 4 = 128x64.
+ * The environment variable LC_GEMM_TILE sets the initial value. */
+int lc_gemm_set_tile(int tile);
+
+/* C[N1,N2] += alpha * A[M,N1]^T . B[M,N2] (f32 C, atomically accumulated; split over M);
+ * if colsum != NULL also colsum[N1] += colsum_scale * sum_m A[m][:] (the bias gradient).
+ * Replaces: the autograd weight- and bias-gradient reductions of adapter down_proj / up_proj
  * (models/clip/adapter.py:38-40, 59-62). */
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
-               long ldb, float alpha, float* C, long ldc);
+               long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale);
 
 /* LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0), fp32 statistics, eps 1e-5.
  * y is bf16 (y_f32 = 0) or f32 (y_f32 = 1); row_idx (optional) gathers input rows.
@@ -116,12 +122,12 @@ int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, co
                    const float* bd, const void* Wu, const float* bu, float scale, float keep,
                    unsigned long long seed, const float* resid, float* xout, long ldx, void* h);
 
-/* Row-local adapter backward: dpre (bf16 [M,64]), dz = gout + dpre Wd (bf16), dbd += sum dpre,
- * dbu += scale * sum gout. WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16).
+/* Row-local adapter backward: dpre (bf16 [M,64]) and dz = gout + dpre Wd (bf16).
+ * WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16). Weight/bias gradients: lc_gemm_tn.
  * Replaces: autograd of adapter.py:59-72. */
 int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
-                   void* dz, long ldz, float* dbd, float* dbu);
+                   void* dz, long ldz);
 
 /* *flag |= any(!isfinite(g))  (GradScaler's inf check, _trainer.py:163, adapter_clip.py:94). */
 int lc_check_finite(hipStream_t stream, long n, const float* g, int* flag);

@@ -19,6 +19,7 @@
 // Grid: one workgroup per output tile, XCD-aware bijective remap so that the tiles an XCD
 // runs are contiguous in (m, n) order and share A row-panels in its L2.
 #include "lc_common.h"
+#include <stdlib.h>
 
 enum {
   EPI_BF16 = 0,        // out0 bf16 = acc*alpha + bias
@@ -27,20 +28,26 @@ enum {
   EPI_GELU = 3,        // out0 bf16 = pre = acc+bias ; out1 bf16 = quick_gelu(pre)
   EPI_GELU_BWD = 4,    // out0 bf16 = (acc*alpha) * quick_gelu'(aux_bf16)
   EPI_BF16_F32 = 5,    // out0 bf16 and out1 f32 of acc*alpha + bias
+  // fused adapter epilogues (internal; adapter.py:59-72 as two skinny GEMMs)
+  EPI_AD_DOWN = 6,     // out0 bf16 = relu(acc + bias) * dropmask(seed, m, n) / keep
+  EPI_AD_UP = 7,       // out0 f32 = aux_f32 + aux2_bf16 + scale * (acc + bias)
+  EPI_AD_MASK = 8,     // out0 bf16 = aux_bf16 > 0 ? alpha * acc / keep : 0
+  EPI_AD_ADD = 9,      // out0 bf16 = aux_bf16 + acc
 };
 
 namespace {
 
 constexpr int BK = 64;
-constexpr int NT = 256;
+
 
 LC_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int ROWS>
+template <int ROWS, int NW>
 LC_DEV void stage_tile(const bf16_t* __restrict__ g, long ld, int row0, int rows_valid, int k0,
                        char* lds, int tid) {
   // ROWS x 64 bf16 tile = ROWS*128 bytes; one wave-instruction moves 8 rows (1 KiB).
-  constexpr int INSTR = ROWS / 8 / 4;  // per wave (4 waves)
+  constexpr int INSTR = ROWS / 8 / NW;  // per wave
+  static_assert(INSTR * 8 * NW == ROWS, "tile rows must split evenly over the waves");
   const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
@@ -58,16 +65,28 @@ LC_DEV bf16x8 read_frag(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + swz(row, chunk) * 16);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
-__global__ void __launch_bounds__(NT, 2)
+template <int N>
+LC_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// BM x BN block tile, WM x WN waves, STAGES-deep LDS ring filled by global_load_lds.
+// Loop body per K-tile t: issue the DMA of tile t+STAGES-1, read fragments of tile t from LDS,
+// MFMA cluster under s_setprio(1), then a COUNTED vmcnt (tile t+1 has landed, later tiles stay
+// in flight) and a raw s_barrier (no implicit vmcnt(0) drain).
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 ? 2 : 1))
 gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
                const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
                float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
-               long ldo1, const void* __restrict__ aux, long ldaux) {
+               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
+  constexpr int NW = WM * WN;
   constexpr int TM = BM / WM / 16;  // 16-row subtiles per wave (activation rows)
   constexpr int TN = BN / WN / 16;  // 16-col subtiles per wave (output features)
   constexpr int STAGE_BYTES = (BM + BN) * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  constexpr int LOADS = (BM + BN) / 8 / NW;  // glds instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -93,17 +112,24 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
   const int nk = K / BK;
   auto stage = [&](int buf, int kt) {
     char* s = smem + buf * STAGE_BYTES;
-    stage_tile<BM>(A, lda, m0, M, kt * BK, s, tid);
-    stage_tile<BN>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
+    stage_tile<BM, NW>(A, lda, m0, M, kt * BK, s, tid);
+    stage_tile<BN, NW>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
   };
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // prologue: STAGES-1 tiles in flight, wait for the first
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s);
+  if (nk >= STAGES - 1) wait_vmcnt<LOADS * (STAGES - 2)>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
 
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const int pre = kt + STAGES - 1;
+    int pbuf = cur + STAGES - 1;
+    if (pbuf >= STAGES) pbuf -= STAGES;
+    if (pre < nk) stage(pbuf, pre);
     const char* sa = smem + cur * STAGE_BYTES;
     const char* sb = sa + BM * 128;
 #pragma unroll
@@ -114,53 +140,124 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
       for (int i = 0; i < TM; ++i) fa[i] = read_frag(sa, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = read_frag(sb, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // tile kt+1 must have landed; tiles up to kt+STAGES-1 may stay in flight
+    if (pre < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
   }
 
-  // Epilogue: lane holds out[m][n..n+3], m = row of activation subtile, n = 4 consecutive cols.
+  // Epilogue through LDS. The swapped MFMA leaves 4 consecutive columns of one row per lane, so
+  // a direct store would touch 16 rows x 64 B per instruction. Each wave instead parks 32 rows
+  // of its accumulator tile in the (now idle) stage ring and reads them back row-contiguous:
+  // every global load/store of the epilogue covers whole 256-B row segments.
+  constexpr int WT_M = BM / WM, WT_N = BN / WN;
+  constexpr int PASS = 32;
+  constexpr int LSTR = WT_N + 4;          // floats per staged row (pad: bank spread)
+  constexpr int LPR = WT_N / 4;           // lanes per row (4 columns each)
+  constexpr int RPI = 64 / LPR;           // rows per read-back instruction
+  static_assert(NW * PASS * LSTR * 4 <= STAGES * STAGE_BYTES, "epilogue staging must fit");
+  float* stg = reinterpret_cast<float*>(smem) + wave * PASS * LSTR;
+  const int lc = (lane % LPR) * 4;
+  const int n = n0 + wn * WT_N + lc;
+  float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (EPI != EPI_GELU_BWD && EPI != EPI_AD_MASK && EPI != EPI_AD_ADD && bias != nullptr)
+    bb = *reinterpret_cast<const float4*>(bias + n);
+  // side inputs (residual / pre-activation / adapter z / h) of a pass are fetched one pass
+  // ahead, before the stores of the current pass: CDNA's vmcnt also counts stores, so a load
+  // issued after them would wait for their acknowledgement.
+  constexpr bool AUXF = (EPI == EPI_RESID || EPI == EPI_AD_UP);
+  constexpr bool AUXB = (EPI == EPI_GELU_BWD || EPI == EPI_AD_MASK || EPI == EPI_AD_ADD);
+  constexpr bool AUX2 = (EPI == EPI_AD_UP);
+  constexpr int NIT = PASS / RPI;
+  float4 pf_f[2][NIT];
+  uint2 pf_b[2][NIT];
+  auto prefetch = [&](int pass, int slot) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    if (m >= M) continue;
+    for (int it = 0; it < NIT; ++it) {
+      long m = m0 + wm * WT_M + pass * PASS + it * RPI + lane / LPR;
+      m = m < M ? m : M - 1;
+      if constexpr (AUXF) pf_f[slot][it] = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n);
+      if constexpr (AUXB) pf_b[slot][it] = *reinterpret_cast<const uint2*>((const bf16_t*)aux + m * ldaux + n);
+      if constexpr (AUX2) pf_b[slot][it] = *reinterpret_cast<const uint2*>((const bf16_t*)ep.aux2 + m * ep.ldaux2 + n);
+    }
+  };
+  if constexpr (AUXF || AUXB) prefetch(0, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
-      float v[4];
+  for (int pass = 0; pass < WT_M / PASS; ++pass) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
-      if (EPI != EPI_GELU_BWD && bias != nullptr) {
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-      }
+    for (int ii = 0; ii < PASS / 16; ++ii)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(stg + (ii * 16 + (lane & 15)) * LSTR + j * 16 + (lane >> 4) * 4) =
+            acc[pass * (PASS / 16) + ii][j];
+    if constexpr (AUXF || AUXB)
+      if (pass + 1 < WT_M / PASS) prefetch(pass + 1, (pass + 1) & 1);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int lr = it * RPI + lane / LPR;
+      const long m = m0 + wm * WT_M + pass * PASS + lr;
+      const f32x4 a4 = *reinterpret_cast<const f32x4*>(stg + lr * LSTR + lc);
+      const float4 xf = pf_f[pass & 1][it];
+      const uint2 xb = pf_b[pass & 1][it];
+      if (m >= M) continue;
+      float v[4] = {a4[0] * alpha + bb.x, a4[1] * alpha + bb.y, a4[2] * alpha + bb.z,
+                    a4[3] * alpha + bb.w};
       if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
-        uint2 pk = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
         if constexpr (EPI == EPI_BF16_F32)
           *reinterpret_cast<float4*>((float*)out1 + m * ldo1 + n) = make_float4(v[0], v[1], v[2], v[3]);
       } else if constexpr (EPI == EPI_F32) {
         *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) = make_float4(v[0], v[1], v[2], v[3]);
       } else if constexpr (EPI == EPI_RESID) {
-        const float4 x = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n);
+        const float4 x = xf;
         *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) =
             make_float4(x.x + v[0], x.y + v[1], x.z + v[2], x.w + v[3]);
       } else if constexpr (EPI == EPI_GELU) {
-        uint2 pk = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
-        uint2 pg = {pack2bf(quick_gelu(v[0]), quick_gelu(v[1])),
-                    pack2bf(quick_gelu(v[2]), quick_gelu(v[3]))};
-        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) = pg;
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) =
+            uint2{pack2bf(quick_gelu(v[0]), quick_gelu(v[1])), pack2bf(quick_gelu(v[2]), quick_gelu(v[3]))};
       } else if constexpr (EPI == EPI_GELU_BWD) {
-        const uint2 a = *reinterpret_cast<const uint2*>((const bf16_t*)aux + m * ldaux + n);
-        float g0 = quick_gelu_grad(bf2f(a.x & 0xffff)), g1 = quick_gelu_grad(bf2f(a.x >> 16));
-        float g2 = quick_gelu_grad(bf2f(a.y & 0xffff)), g3 = quick_gelu_grad(bf2f(a.y >> 16));
-        uint2 pk = {pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) = pk;
+        const uint2 a = xb;
+        const float g0 = quick_gelu_grad(bf2f(a.x & 0xffff)), g1 = quick_gelu_grad(bf2f(a.x >> 16));
+        const float g2 = quick_gelu_grad(bf2f(a.y & 0xffff)), g3 = quick_gelu_grad(bf2f(a.y >> 16));
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
+      } else if constexpr (EPI == EPI_AD_DOWN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f) * drop_mul(ep.seed, m, n + r, ep.keep);
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      } else if constexpr (EPI == EPI_AD_UP) {
+        const float4 x = xf;
+        const uint2 zz = xb;
+        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) =
+            make_float4(x.x + bf2f(zz.x & 0xffff) + ep.scale * v[0],
+                        x.y + bf2f(zz.x >> 16) + ep.scale * v[1],
+                        x.z + bf2f(zz.y & 0xffff) + ep.scale * v[2],
+                        x.w + bf2f(zz.y >> 16) + ep.scale * v[3]);
+      } else if constexpr (EPI == EPI_AD_MASK) {
+        const uint2 hv = xb;
+        const float inv = 1.0f / ep.keep;
+        const float hh[4] = {bf2f(hv.x & 0xffff), bf2f(hv.x >> 16), bf2f(hv.y & 0xffff), bf2f(hv.y >> 16)};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = hh[r] > 0.f ? v[r] * inv : 0.f;
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      } else if constexpr (EPI == EPI_AD_ADD) {
+        const uint2 gg = xb;
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(bf2f(gg.x & 0xffff) + v[0], bf2f(gg.x >> 16) + v[1]),
+                  pack2bf(bf2f(gg.y & 0xffff) + v[2], bf2f(gg.y >> 16) + v[3])};
       }
     }
   }
@@ -182,8 +279,9 @@ LC_DEV bf16x4 tr_read(const char* lds, int row, int col) {
 __global__ void __launch_bounds__(256)
 gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__ A, long lda,
                const bf16_t* __restrict__ B, long ldb, float alpha, float* __restrict__ C,
-               long ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TN_BM * 128];
+               long ldc, float* __restrict__ colsum, float colsum_scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TN_BM * 128 + 4 * 64 * 4];
+  float* red = reinterpret_cast<float*>(smem + 2 * 2 * TN_BM * 128);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wa = wave >> 1, wb = wave & 1;
   const int tiles_n2 = N2 / 64;
@@ -192,6 +290,10 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
   const int mbeg = blockIdx.y * chunk_rows;
   const int mend = min(M, mbeg + chunk_rows);
   if (mbeg >= mend) return;
+  // bias gradient fused in: column sums of the A tile (only the t2 == 0 column of workgroups,
+  // so every A column is summed exactly once)
+  const bool do_cs = colsum != nullptr && t2 == 0;
+  float cs = 0.f;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -231,6 +333,11 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
       }
       __syncthreads();
     }
+    if (do_cs) {
+      const bf16_t* col = reinterpret_cast<const bf16_t*>(sa) + (tid & 63);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cs += bf2f(col[((tid >> 6) + 4 * i) * 64]);
+    }
     const int g = lane >> 4, t = lane & 15;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -254,6 +361,11 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if (do_cs) {
+    red[tid] = cs;
+    __syncthreads();
+    if (tid < 64) atomicAdd(colsum + c1 + tid, colsum_scale * (red[tid] + red[tid + 64] + red[tid + 128] + red[tid + 192]));
+  }
   // acc[i][j]: lane holds D[n1 = 4g + r][n2 = t] of subtile (i, j)
   const int g = lane >> 4, t = lane & 15;
 #pragma unroll
@@ -268,16 +380,16 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
       }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGES>
 int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
-              void* o1, long l1, const void* aux, long la) {
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  dim3 grid(tiles), block(NT);
-#define LC_NT_CASE(E)                                                                        \
-  case E:                                                                                    \
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, E>), grid, block, 0, st, M, N, K, A,  \
-                       lda, B, ldb, bias, alpha, o0, l0, o1, l1, aux, la);                   \
+  dim3 grid(tiles), block(64 * WM * WN);
+#define LC_NT_CASE(E)                                                                         \
+  case E:                                                                                     \
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, STAGES, E>), grid, block, 0, st, M, N, \
+                       K, A, lda, B, ldb, bias, alpha, o0, l0, o1, l1, aux, la, ep);          \
     break;
   switch (epi) {
     LC_NT_CASE(EPI_BF16)
@@ -286,6 +398,10 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
     LC_NT_CASE(EPI_GELU)
     LC_NT_CASE(EPI_GELU_BWD)
     LC_NT_CASE(EPI_BF16_F32)
+    LC_NT_CASE(EPI_AD_DOWN)
+    LC_NT_CASE(EPI_AD_UP)
+    LC_NT_CASE(EPI_AD_MASK)
+    LC_NT_CASE(EPI_AD_ADD)
     default:
       return LC_EINVAL;
   }
@@ -293,7 +409,57 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
   LC_LAUNCH_RET();
 }
 
+// tile-shape selector (env LC_GEMM_TILE forces one for experiments: 0 auto, 1 = 128x128x2,
+// 2 = 256x128x3, 3 = 256x256x2, 4 = 128x64x2)
+int g_force_tile = -1;
+
 }  // namespace
+
+extern "C" {
+
+}  // extern "C"
+
+int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep) {
+  LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
+  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
+  LC_CHECK_ARG(ldo0 % 4 == 0 && ldo0 >= N);
+  LC_CHECK_ARG(epi >= 0 && epi <= 9);
+  if (epi == EPI_GELU || epi == EPI_BF16_F32) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
+  if (epi == EPI_RESID || epi == EPI_GELU_BWD || epi >= EPI_AD_UP)
+    LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 4 == 0);
+  if (epi == EPI_AD_UP) LC_CHECK_ARG(ep.aux2 != nullptr && ep.ldaux2 >= N && ep.ldaux2 % 4 == 0);
+  auto a = static_cast<const bf16_t*>(A);
+  auto b = static_cast<const bf16_t*>(B);
+  if (g_force_tile < 0) {
+    const char* e = getenv("LC_GEMM_TILE");
+    g_force_tile = e ? atoi(e) : 0;
+  }
+  int tile = g_force_tile;
+  if (tile == 0) {
+    // measured on the ViT-B/16 step shapes (tools/bench_gemm.py): 256x256 for the wide
+    // N >= 2048 GEMMs, 128x128 at 2 workgroups/CU for N = 768 (better wave quantisation)
+    if (N % 128 != 0) tile = 4;
+    else if (M >= 4096 && N % 256 == 0 && N >= 2048) tile = 3;
+    else tile = 1;
+  }
+  if ((tile == 3 && N % 256) || ((tile == 1 || tile == 2) && N % 128)) tile = 4;
+  switch (tile) {
+    case 1:
+      return launch_nt<128, 128, 2, 2, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                          ldo0, out1, ldo1, aux, ldaux, ep);
+    case 2:
+      return launch_nt<256, 128, 4, 2, 3>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                          ldo0, out1, ldo1, aux, ldaux, ep);
+    case 3:
+      return launch_nt<256, 256, 2, 4, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                          ldo0, out1, ldo1, aux, ldaux, ep);
+    default:
+      return launch_nt<128, 64, 4, 1, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                         ldo0, out1, ldo1, aux, ldaux, ep);
+  }
+}
 
 extern "C" {
 
@@ -301,23 +467,20 @@ extern "C" {
 int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux) {
-  LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
-  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
-  LC_CHECK_ARG(ldo0 % 4 == 0 && ldo0 >= N);
   LC_CHECK_ARG(epi >= 0 && epi <= 5);
-  if (epi == EPI_GELU || epi == EPI_BF16_F32) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
-  if (epi == EPI_RESID || epi == EPI_GELU_BWD) LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 4 == 0);
-  auto a = static_cast<const bf16_t*>(A);
-  auto b = static_cast<const bf16_t*>(B);
-  if (N % 128 == 0)
-    return launch_nt<128, 128, 2, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
-                                     ldo0, out1, ldo1, aux, ldaux);
-  return launch_nt<128, 64, 4, 1>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0,
-                                  out1, ldo1, aux, ldaux);
+  EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0};
+  return lc_gemm_nt_ex(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                       aux, ldaux, ep);
+}
+
+int lc_gemm_set_tile(int tile) {
+  LC_CHECK_ARG(tile >= 0 && tile <= 4);
+  g_force_tile = tile;
+  return LC_OK;
 }
 
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
-               long ldb, float alpha, float* C, long ldc) {
+               long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale) {
   LC_CHECK_ARG(M > 0 && N1 % 64 == 0 && N2 % 64 == 0 && N1 > 0 && N2 > 0);
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= N1 && ldb >= N2 && ldc >= N2);
   const int tiles = (N1 / 64) * (N2 / 64);
@@ -330,7 +493,7 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
   dim3 grid(tiles, splits), block(256);
   hipLaunchKernelGGL(gemm_tn_kernel, grid, block, 0, stream, M, N1, N2, chunk,
                      static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(B), ldb, alpha,
-                     C, ldc);
+                     C, ldc, colsum, colsum_scale);
   LC_LAUNCH_RET();
 }
 

@@ -62,6 +62,27 @@ LC_DEV uint32_t lc_hash(uint64_t seed, uint64_t idx) {
   return (uint32_t)(z >> 32);
 }
 
+// Dropout multiplier for adapter bottleneck element (row m, column j): 1/keep or 0.
+LC_DEV float drop_mul(uint64_t seed, long m, int j, float keep) {
+  if (keep >= 1.0f) return 1.0f;
+  const uint32_t hsh = lc_hash(seed, (uint64_t)m * 64 + j);
+  const float u = (hsh >> 8) * (1.0f / 16777216.0f);
+  return u < keep ? 1.0f / keep : 0.0f;
+}
+
+// Extra epilogue operands of the fused GEMM epilogues (internal).
+struct EpiParams {
+  const void* aux2;  // second side input (bf16), e.g. the adapter input z
+  long ldaux2;
+  float scale;       // adapter scalar
+  float keep;        // 1 - dropout p
+  uint64_t seed;     // dropout mask seed
+};
+
+// Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).
+int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep);
 
 #define LC_CHECK_ARG(cond) \
   do {                     \

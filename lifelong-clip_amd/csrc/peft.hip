@@ -185,156 +185,6 @@ LC_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return r;
 }
 
-LC_DEV float drop_mul(uint64_t seed, long m, int j, float keep) {
-  if (keep >= 1.0f) return 1.0f;
-  const uint32_t hsh = lc_hash(seed, (uint64_t)m * AD_H + j);
-  const float u = (hsh >> 8) * (1.0f / 16777216.0f);
-  return u < keep ? 1.0f / keep : 0.0f;
-}
-
-__global__ void __launch_bounds__(256)
-adapter_fwd_kernel(int M, int Dw, const bf16_t* __restrict__ z, long ldz,
-                   const bf16_t* __restrict__ Wd, const float* __restrict__ bd,
-                   const bf16_t* __restrict__ Wu, const float* __restrict__ bu, float scale,
-                   float keep, uint64_t seed, const float* __restrict__ resid,
-                   float* __restrict__ xout, long ldx, bf16_t* __restrict__ hout) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, t = lane & 15;
-  const int m = blockIdx.x * 64 + w * 16 + t;
-  const bool ok = m < M;
-  const long mr = ok ? m : (M - 1);
-  const bf16_t* zr = z + mr * ldz;
-
-  f32x4 dn[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dn[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < Dw; k0 += 32) {
-    const bf16x8 zb = *reinterpret_cast<const bf16x8*>(zr + k0 + 8 * g);
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const bf16x8 wa = *reinterpret_cast<const bf16x8*>(Wd + (long)(jt * 16 + t) * Dw + k0 + 8 * g);
-      dn[jt] = mfma16(wa, zb, dn[jt]);
-    }
-  }
-  // lane holds D[j = jt*16 + 4g + r][m]
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = jt * 16 + 4 * g + r;
-      const float v = fmaxf(dn[jt][r] + bd[j], 0.f) * drop_mul(seed, m, j, keep);
-      dn[jt][r] = __uint_as_float((uint32_t)f2bf(v) << 16);  // round to the stored bf16 value
-    }
-  if (ok) {
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-      *reinterpret_cast<uint2*>(hout + (long)m * AD_H + jt * 16 + 4 * g) =
-          uint2{pack2bf(dn[jt][0], dn[jt][1]), pack2bf(dn[jt][2], dn[jt][3])};
-  }
-  const bf16x8 hb0 = pack8(dn[0], dn[1]);  // k-step 0 (j 0..31)
-  const bf16x8 hb1 = pack8(dn[2], dn[3]);  // k-step 1 (j 32..63)
-  for (int nt = 0; nt < Dw / 16; ++nt) {
-    const bf16_t* wrow = Wu + (long)(nt * 16 + t) * AD_H;
-    f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
-    u = mfma16(load_perm(wrow, 0, g), hb0, u);
-    u = mfma16(load_perm(wrow, 1, g), hb1, u);
-    if (ok) {
-      const int n = nt * 16 + 4 * g;
-      const float4 rs = *reinterpret_cast<const float4*>(resid + (long)m * ldx + n);
-      const uint2 zz = *reinterpret_cast<const uint2*>(zr + n);
-      const float4 bb = *reinterpret_cast<const float4*>(bu + n);
-      float4 o;
-      o.x = rs.x + bf2f(zz.x & 0xffff) + scale * (u[0] + bb.x);
-      o.y = rs.y + bf2f(zz.x >> 16) + scale * (u[1] + bb.y);
-      o.z = rs.z + bf2f(zz.y & 0xffff) + scale * (u[2] + bb.z);
-      o.w = rs.w + bf2f(zz.y >> 16) + scale * (u[3] + bb.w);
-      *reinterpret_cast<float4*>(xout + (long)m * ldx + n) = o;
-    }
-  }
-}
-
-// Backward of out = z + scale*(h Wu^T + bu), h = drop(relu(z Wd^T + bd)), given gout:
-//   dh^T[j][m] = scale * sum_n WuT[j][n] gout[m][n]
-//   dpre = dh * (h > 0) / keep            -> dpre_out (bf16), dbd += sum_m dpre
-//   dz^T[n][m] = sum_j WdT[n][j] dpre[m][j]; dz = gout + dz   -> dz_out (bf16)
-//   dbu += scale * sum_m gout
-// (dWu = scale * gout^T h and dWd = dpre^T z are done by lc_gemm_tn.)
-__global__ void __launch_bounds__(256)
-adapter_bwd_kernel(int M, int Dw, const bf16_t* __restrict__ gout, long ldg,
-                   const bf16_t* __restrict__ h, const bf16_t* __restrict__ WuT,
-                   const bf16_t* __restrict__ WdT, float scale, float keep,
-                   bf16_t* __restrict__ dpre_out, bf16_t* __restrict__ dz_out, long ldz,
-                   float* __restrict__ dbd, float* __restrict__ dbu) {
-  __shared__ float colsum[1024];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, t = lane & 15;
-  const int m = blockIdx.x * 64 + w * 16 + t;
-  const bool ok = m < M;
-  const long mr = ok ? m : (M - 1);
-  const bf16_t* gr = gout + mr * ldg;
-  for (int i = tid; i < Dw; i += 256) colsum[i] = 0.f;
-
-  f32x4 dh[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) dh[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < Dw; k0 += 32) {
-    const bf16x8 gb = *reinterpret_cast<const bf16x8*>(gr + k0 + 8 * g);
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-      const bf16x8 wa = *reinterpret_cast<const bf16x8*>(WuT + (long)(jt * 16 + t) * Dw + k0 + 8 * g);
-      dh[jt] = mfma16(wa, gb, dh[jt]);
-    }
-  }
-  float dbd_loc[4][4];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt) {
-    const uint2 hv = *reinterpret_cast<const uint2*>(h + mr * AD_H + jt * 16 + 4 * g);
-    const float hh[4] = {bf2f(hv.x & 0xffff), bf2f(hv.x >> 16), bf2f(hv.y & 0xffff), bf2f(hv.y >> 16)};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = (ok && hh[r] > 0.f) ? dh[jt][r] * scale / keep : 0.f;
-      v = __uint_as_float((uint32_t)f2bf(v) << 16);
-      dh[jt][r] = v;
-      dbd_loc[jt][r] = v;
-    }
-    if (ok)
-      *reinterpret_cast<uint2*>(dpre_out + (long)m * AD_H + jt * 16 + 4 * g) =
-          uint2{pack2bf(dh[jt][0], dh[jt][1]), pack2bf(dh[jt][2], dh[jt][3])};
-  }
-  // dbd: reduce over the 16 rows (lanes t) of this wave, then atomics
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = dbd_loc[jt][r];
-      v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4); v += __shfl_xor(v, 8);
-      if (t == 0) atomicAdd(dbd + jt * 16 + 4 * g + r, v);
-    }
-  __syncthreads();  // colsum zeroed
-  const bf16x8 pb0 = pack8(dh[0], dh[1]);
-  const bf16x8 pb1 = pack8(dh[2], dh[3]);
-  for (int nt = 0; nt < Dw / 16; ++nt) {
-    const bf16_t* wrow = WdT + (long)(nt * 16 + t) * AD_H;
-    f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
-    u = mfma16(load_perm(wrow, 0, g), pb0, u);
-    u = mfma16(load_perm(wrow, 1, g), pb1, u);
-    const int n = nt * 16 + 4 * g;
-    const uint2 gg = *reinterpret_cast<const uint2*>(gr + n);
-    const float g4[4] = {bf2f(gg.x & 0xffff), bf2f(gg.x >> 16), bf2f(gg.y & 0xffff), bf2f(gg.y >> 16)};
-    if (ok)
-      *reinterpret_cast<uint2*>(dz_out + (long)m * ldz + n) =
-          uint2{pack2bf(g4[0] + u[0], g4[1] + u[1]), pack2bf(g4[2] + u[2], g4[3] + u[3])};
-    // column sums of gout over this wave's 16 rows
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float v = ok ? g4[r] : 0.f;
-      v += __shfl_xor(v, 1); v += __shfl_xor(v, 2); v += __shfl_xor(v, 4); v += __shfl_xor(v, 8);
-      if (t == 0) atomicAdd(&colsum[n + r], v);
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < Dw; i += 256) atomicAdd(dbu + i, scale * colsum[i]);
-}
 
 // ---------------------------------------------------------------------------- AdamW
 __global__ void finite_kernel(long n, const float* __restrict__ g, int* __restrict__ flag) {
@@ -403,26 +253,36 @@ int lc_lora_grad(hipStream_t st, int M, int N, int K, int r, const void* dY, lon
   LC_LAUNCH_RET();
 }
 
+// The adapter as two skinny GEMMs through lc_gemm_nt's LDS-staged MFMA template (the weights
+// are staged once per workgroup by global_load_lds instead of being re-read by every wave):
+//   h    = drop(relu(z Wd^T + bd))                 [M,64]  N = 64,  K = D
+//   xout = resid + z + scale * (h Wu^T + bu)       [M,D]   N = D,   K = 64
 int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
                    const float* bd, const void* Wu, const float* bu, float scale, float keep,
                    unsigned long long seed, const float* resid, float* xout, long ldx, void* hout) {
-  LC_CHECK_ARG(M > 0 && D % 32 == 0 && D % 16 == 0 && ldz % 8 == 0 && ldx % 4 == 0);
+  LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldz % 8 == 0 && ldx % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  hipLaunchKernelGGL(adapter_fwd_kernel, dim3((M + 63) / 64), dim3(256), 0, st, M, D,
-                     (const bf16_t*)z, ldz, (const bf16_t*)Wd, bd, (const bf16_t*)Wu, bu, scale,
-                     keep, (uint64_t)seed, resid, xout, ldx, (bf16_t*)hout);
-  LC_LAUNCH_RET();
+  EpiParams ep{z, ldz, scale, keep, (uint64_t)seed};
+  int rc = lc_gemm_nt_ex(st, 6 /*EPI_AD_DOWN*/, M, AD_H, D, z, ldz, Wd, D, bd, 1.0f, hout, AD_H,
+                         nullptr, 0, nullptr, 0, ep);
+  if (rc) return rc;
+  return lc_gemm_nt_ex(st, 7 /*EPI_AD_UP*/, M, D, AD_H, hout, AD_H, Wu, AD_H, bu, 1.0f, xout, ldx,
+                       nullptr, 0, resid, ldx, ep);
 }
 
+//   dpre = (h > 0) ? scale * (gout Wu) / keep : 0    [M,64]  N = 64, K = D   (B = Wu^T)
+//   dz   = gout + dpre Wd                            [M,D]   N = D,  K = 64  (B = Wd^T)
 int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, const void* h,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
-                   void* dz, long ldz, float* dbd, float* dbu) {
-  LC_CHECK_ARG(M > 0 && D % 32 == 0 && D <= 1024 && ldg % 8 == 0 && ldz % 4 == 0);
+                   void* dz, long ldz) {
+  LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  hipLaunchKernelGGL(adapter_bwd_kernel, dim3((M + 63) / 64), dim3(256), 0, st, M, D,
-                     (const bf16_t*)gout, ldg, (const bf16_t*)h, (const bf16_t*)WuT,
-                     (const bf16_t*)WdT, scale, keep, (bf16_t*)dpre, (bf16_t*)dz, ldz, dbd, dbu);
-  LC_LAUNCH_RET();
+  EpiParams ep{nullptr, 0, scale, keep, 0};
+  int rc = lc_gemm_nt_ex(st, 8 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
+                         AD_H, nullptr, 0, h, AD_H, ep);
+  if (rc) return rc;
+  return lc_gemm_nt_ex(st, 9 /*EPI_AD_ADD*/, M, D, AD_H, dpre, AD_H, WdT, AD_H, nullptr, 1.0f, dz,
+                       ldz, nullptr, 0, gout, ldg, ep);
 }
 
 int lc_check_finite(hipStream_t st, long n, const float* g, int* flag) {

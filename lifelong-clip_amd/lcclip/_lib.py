@@ -20,7 +20,8 @@ P = c_void_p
 SIGNATURES = {
     "lc_gemm_nt": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_float, P, c_long, P,
                    c_long, P, c_long],
-    "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long],
+    "lc_gemm_set_tile": [c_int],
+    "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float],
     "lc_layernorm_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_int, c_long, P, P],
     "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
     "lc_patchify": [P, c_int, c_int, c_int, P, P],
@@ -34,7 +35,7 @@ SIGNATURES = {
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
     "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
                        c_long, P],
-    "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long, P, P],
+    "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long],
     "lc_check_finite": [P, c_long, P, P],
     "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P],
     "lc_l2norm_rows": [P, c_int, c_int, P, c_long, P, P],

@@ -240,10 +240,11 @@ class BlockStack:
         ad = blk.adaptmlp
         M = gout.shape[0]
         dpre = _empty((M, ad.down_size), BF16, gout.device)
-        ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz,
-                        self._grad(grads, ad.down_proj.bias), self._grad(grads, ad.up_proj.bias))
-        ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale)
-        ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0)
+        ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz)
+        ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale,
+                    colsum=self._grad(grads, ad.up_proj.bias), colsum_scale=ad.scale)
+        ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0,
+                    colsum=self._grad(grads, ad.down_proj.bias), colsum_scale=1.0)
         return dz
 
     def _lora_grad(self, dY, X, A, B, scaling, grads):

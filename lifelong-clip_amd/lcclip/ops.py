@@ -36,8 +36,8 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
     return out0
 
 
-def gemm_tn(A, B, C, alpha=1.0):
-    """C[N1,N2] += alpha * A[M,N1]^T @ B[M,N2] (C f32)."""
+def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
+    """C[N1,N2] += alpha * A[M,N1]^T @ B[M,N2] (C f32); colsum[N1] += colsum_scale * sum_m A."""
     _rowmajor(A, BF16, "A")
     _rowmajor(B, BF16, "B")
     _rowmajor(C, F32, "C")
@@ -45,8 +45,10 @@ def gemm_tn(A, B, C, alpha=1.0):
     N2 = B.shape[1]
     if B.shape[0] != M or C.shape[0] != N1 or C.shape[1] != N2:
         raise ValueError("gemm_tn shape mismatch")
+    if colsum is not None and (colsum.dtype != F32 or colsum.numel() != N1):
+        raise ValueError("colsum must be f32 [N1]")
     call("lc_gemm_tn", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
-         float(alpha), ptr(C), C.stride(0))
+         float(alpha), ptr(C), C.stride(0), ptr(colsum), float(colsum_scale))
     return C
 
 
@@ -143,10 +145,10 @@ def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h):
          xout.stride(0), ptr(h))
 
 
-def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz, dbd, dbu):
+def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
     M, D = gout.shape
     call("lc_adapter_bwd", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
-         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz), dz.stride(0), ptr(dbd), ptr(dbu))
+         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz), dz.stride(0))
 
 
 def check_finite(g, flag):
