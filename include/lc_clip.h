@@ -47,9 +47,14 @@ int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, 
                void* out1, long ldo1, const void* aux, long ldaux);
 
 /* Tile-shape override for lc_gemm_nt (tuning): 0 = automatic, 1 = 128x128 (4 waves),
- * 2 = 256x128 (8 waves, 3-stage LDS ring), 3 = 256x256 (8 waves, 2 stages), 4 = 128x64.
+ * 2 = 256x128 (8 waves, 3-stage LDS ring), 3 = 256x256 (8 waves, 2 stages), 4 = 128x64,
+ * 5 = 256x256 ping-pong (8 waves in two staggered groups, 4-slot k-half LDS ring), 6 = same.
  * The environment variable LC_GEMM_TILE sets the initial value. */
 int lc_gemm_set_tile(int tile);
+
+/* Diagnostic: when p != NULL, the ping-pong GEMM stores s_memtime stamps of its segments
+ * (workgroup 0, waves 0 and 4) to p[512] (tools/gemm_trace.py). NULL disables (default). */
+int lc_gemm_set_debug(unsigned long long* p);
 
 /* C[N1,N2] += alpha * A[M,N1]^T . B[M,N2] (f32 C, atomically accumulated; split over M);
  * if colsum != NULL also colsum[N1] += colsum_scale * sum_m A[m][:] (the bias gradient).

@@ -71,99 +71,26 @@ LC_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// BM x BN block tile, WM x WN waves, STAGES-deep LDS ring filled by global_load_lds.
-// Loop body per K-tile t: issue the DMA of tile t+STAGES-1, read fragments of tile t from LDS,
-// MFMA cluster under s_setprio(1), then a COUNTED vmcnt (tile t+1 has landed, later tiles stay
-// in flight) and a raw s_barrier (no implicit vmcnt(0) drain).
-template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
-__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 ? 2 : 1))
-gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
-               const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
-               float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
-               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
-  constexpr int NW = WM * WN;
-  constexpr int TM = BM / WM / 16;  // 16-row subtiles per wave (activation rows)
-  constexpr int TN = BN / WN / 16;  // 16-col subtiles per wave (output features)
-  constexpr int STAGE_BYTES = (BM + BN) * 128;
-  constexpr int LOADS = (BM + BN) / 8 / NW;  // glds instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
-
+// Epilogue shared by the GEMM kernels: acc holds the swapped MFMA layout (lane: 4 consecutive
+// columns n of one row m per 16x16 subtile).
+template <int BM, int BN, int WM, int WN, int EPI, int TM, int TN>
+LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0, int n0, int M,
+                       const float* __restrict__ bias, float alpha, void* __restrict__ out0,
+                       long ldo0, void* __restrict__ out1, long ldo1, const void* __restrict__ aux,
+                       long ldaux, const EpiParams& ep) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-
-  // XCD-aware bijective block remap.
-  const int tiles_n = N / BN;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {
-    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
-  }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  auto stage = [&](int buf, int kt) {
-    char* s = smem + buf * STAGE_BYTES;
-    stage_tile<BM, NW>(A, lda, m0, M, kt * BK, s, tid);
-    stage_tile<BN, NW>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
-  };
-
-  // prologue: STAGES-1 tiles in flight, wait for the first
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, s);
-  if (nk >= STAGES - 1) wait_vmcnt<LOADS * (STAGES - 2)>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int pre = kt + STAGES - 1;
-    int pbuf = cur + STAGES - 1;
-    if (pbuf >= STAGES) pbuf -= STAGES;
-    if (pre < nk) stage(pbuf, pre);
-    const char* sa = smem + cur * STAGE_BYTES;
-    const char* sb = sa + BM * 128;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = ks * 4 + (lane >> 4);
-      bf16x8 fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = read_frag(sa, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = read_frag(sb, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    // tile kt+1 must have landed; tiles up to kt+STAGES-1 may stay in flight
-    if (pre < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    cur = cur + 1 == STAGES ? 0 : cur + 1;
-  }
-
-  // Epilogue through LDS. The swapped MFMA leaves 4 consecutive columns of one row per lane, so
+  constexpr int NW = WM * WN;
+  // Through LDS. The swapped MFMA leaves 4 consecutive columns of one row per lane, so
   // a direct store would touch 16 rows x 64 B per instruction. Each wave instead parks 32 rows
   // of its accumulator tile in the (now idle) stage ring and reads them back row-contiguous:
   // every global load/store of the epilogue covers whole 256-B row segments.
   constexpr int WT_M = BM / WM, WT_N = BN / WN;
-  constexpr int PASS = 32;
+  constexpr int PASS = (WT_M % 32 == 0) ? 32 : 16;
   constexpr int LSTR = WT_N + 4;          // floats per staged row (pad: bank spread)
   constexpr int LPR = WT_N / 4;           // lanes per row (4 columns each)
   constexpr int RPI = 64 / LPR;           // rows per read-back instruction
-  static_assert(NW * PASS * LSTR * 4 <= STAGES * STAGE_BYTES, "epilogue staging must fit");
+  (void)smem_bytes;
   float* stg = reinterpret_cast<float*>(smem) + wave * PASS * LSTR;
   const int lc = (lane % LPR) * 4;
   const int n = n0 + wn * WT_N + lc;
@@ -261,6 +188,231 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
       }
     }
   }
+}
+
+// BM x BN block tile, WM x WN waves, STAGES-deep LDS ring filled by global_load_lds.
+// Loop body per K-tile t: issue the DMA of tile t+STAGES-1, read fragments of tile t from LDS,
+// MFMA cluster under s_setprio(1), then a COUNTED vmcnt (tile t+1 has landed, later tiles stay
+// in flight) and a raw s_barrier (no implicit vmcnt(0) drain).
+template <int BM, int BN, int WM, int WN, int STAGES, int EPI>
+__global__ void __launch_bounds__(64 * WM * WN, (WM * WN == 4 ? 2 : 1))
+gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
+               const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
+               float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
+               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM / 16;  // 16-row subtiles per wave (activation rows)
+  constexpr int TN = BN / WN / 16;  // 16-col subtiles per wave (output features)
+  constexpr int STAGE_BYTES = (BM + BN) * 128;
+  constexpr int LOADS = (BM + BN) / 8 / NW;  // glds instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  // XCD-aware bijective block remap.
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  auto stage = [&](int buf, int kt) {
+    char* s = smem + buf * STAGE_BYTES;
+    stage_tile<BM, NW>(A, lda, m0, M, kt * BK, s, tid);
+    stage_tile<BN, NW>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
+  };
+
+  // prologue: STAGES-1 tiles in flight, wait for the first
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s, s);
+  if (nk >= STAGES - 1) wait_vmcnt<LOADS * (STAGES - 2)>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int pre = kt + STAGES - 1;
+    int pbuf = cur + STAGES - 1;
+    if (pbuf >= STAGES) pbuf -= STAGES;
+    if (pre < nk) stage(pbuf, pre);
+    const char* sa = smem + cur * STAGE_BYTES;
+    const char* sb = sa + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = read_frag(sa, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = read_frag(sb, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    // tile kt+1 must have landed; tiles up to kt+STAGES-1 may stay in flight
+    if (pre < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    cur = cur + 1 == STAGES ? 0 : cur + 1;
+  }
+
+  store_tile<BM, BN, WM, WN, EPI>(acc, smem, STAGES * STAGE_BYTES, m0, n0, M, bias, alpha, out0,
+                                  ldo0, out1, ldo1, aux, ldaux, ep);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong GEMM (BM x BN = 256 x 256 or 128 x 256..., 8 waves as 2 x 4).
+// Waves 0-3 (group 0) and 4-7 (group 1) place one wave of each group on every SIMD. The groups
+// are staggered by one s_barrier, so each SIMD alternates: one wave runs an MFMA segment while
+// its partner runs a LOAD segment (ds_read of its fragments + global_load_lds prefetch).
+// K is consumed in 32-deep halves through a 4-slot LDS ring (slot = A [BM][32] + B [BN][32]
+// bf16, 64-B rows); the DMA of half h+3 is issued in the LOAD segment of half h, so a half has
+// three segments to land. Row swizzle for conflict-free ds_read_b128 on 64-B rows:
+// chunk' = chunk ^ (((row >> 3) & 1) << 1).
+// Hazards (every wave): RAW — a wave's own DMA of half h+1 is retired by the counted vmcnt at
+// the end of its LOAD(h); both groups' LOAD(h) precede the barrier that precedes LOAD(h+1) of
+// either group. WAR — slot (h+3)%4 == (h-1)%4 was last read in LOAD(h-1) of both groups, whose
+// lgkmcnt(0) precedes the barriers in front of LOAD(h) of either group.
+LC_DEV int swz64(int row, int chunk) { return chunk ^ (((row >> 3) & 1) << 1); }
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
+               const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
+               float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
+               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 8 x 4 subtiles per wave
+  constexpr int SLOT = (BM + BN) * 64;                 // one k-half: 32 KiB
+  constexpr int NSLOT = 4;
+  constexpr int PIECES = (BM + BN) / 16 / 8;           // 1-KiB DMA pieces per wave per half (4)
+  constexpr int P_LOAD = 2;                            // issued in the LOAD segment
+  constexpr int P_COMP = PIECES - P_LOAD;              // interleaved into the MFMA segment
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;  // wm = group
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nh = K / 32;
+  // piece p of this wave = 16-row block p*8 + wave of half h (A blocks 0..15, B blocks 16..31)
+  auto dma_piece = [&](int h, int p) {
+    const int blk = p * 8 + wave;
+    char* sl = smem + (h % NSLOT) * SLOT;
+    const bool isA = blk < BM / 16;
+    const int b = isA ? blk : blk - BM / 16;
+    const int r = b * 16 + (lane >> 2);
+    const int c = swz64(r, lane & 3);
+    const int rows_valid = isA ? M : N;
+    int gr = (isA ? m0 : n0) + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    const bf16_t* src = isA ? A + (long)gr * lda : B + (long)gr * ldb;
+    glds16(src + h * 32 + c * 8, sl + (isA ? 0 : BM * 64) + b * 1024);
+  };
+  auto dma_half = [&](int h) {
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) dma_piece(h, p);
+  };
+  const bool diag = ep.dbg != nullptr && blockIdx.x == 0 && (wave == 0 || wave == 4) && lane == 0;
+  auto stamp = [&](int idx) {
+    if (diag && idx < 256) {
+      unsigned long long t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      ep.dbg[(wave / 4) * 256 + idx] = t;
+    }
+  };
+
+  // prologue: halves 0..2 in flight; wait for this wave's part of half 0
+  dma_half(0);
+  if (nh > 1) dma_half(1);
+  if (nh > 2) dma_half(2);
+  if (nh > 2) wait_vmcnt<2 * PIECES>();
+  else if (nh > 1) wait_vmcnt<PIECES>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // stagger group 1 by one segment
+
+  const int g = lane >> 4, t = lane & 15;
+  for (int h = 0; h < nh; ++h) {
+    stamp(4 * h);
+    // ---------------- LOAD segment: fragments of half h + the first DMA pieces of half h+3
+    // (slot (h+3)%4 == (h-1)%4 was last read in LOAD(h-1) of both groups)
+    const char* sa = smem + (h % NSLOT) * SLOT;
+    const char* sb = sa + BM * 64;
+    bf16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * (BM / WM) + i * 16 + t;
+      fa[i] = *reinterpret_cast<const bf16x8*>(sa + r * 64 + swz64(r, g) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int r = wn * (BN / WN) + j * 16 + t;
+      fb[j] = *reinterpret_cast<const bf16x8*>(sb + r * 64 + swz64(r, g) * 16);
+    }
+    const bool pre = h + 3 < nh;
+    if (pre) {
+#pragma unroll
+      for (int p = 0; p < P_LOAD; ++p) dma_piece(h + 3, p);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stamp(4 * h + 1);
+    // this wave's DMA of half h+1 must have landed before the barrier in front of LOAD(h+1);
+    // in flight behind it: half h+2 (all pieces) and the pieces of h+3 issued just now
+    if (pre) wait_vmcnt<PIECES + P_LOAD>();
+    else if (h + 2 < nh) wait_vmcnt<PIECES>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    stamp(4 * h + 2);
+    // ---------------- COMPUTE segment (remaining DMA pieces in the MFMA issue gaps)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+      if (P_COMP > 0 && pre && (i * P_COMP) / TM != ((i + 1) * P_COMP) / TM)
+        dma_piece(h + 3, P_LOAD + (i * P_COMP) / TM);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    stamp(4 * h + 3);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
+  store_tile<BM, BN, WM, WN, EPI>(acc, smem, NSLOT * SLOT, m0, n0, M, bias, alpha, out0, ldo0,
+                                  out1, ldo1, aux, ldaux, ep);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -409,9 +561,38 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
   LC_LAUNCH_RET();
 }
 
+int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
+              const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  dim3 grid(tiles), block(512);
+#define LC_PP_CASE(E)                                                                          \
+  case E:                                                                                      \
+    hipLaunchKernelGGL((gemm_pp_kernel<E>), grid, block, 0, st, M, N, K, A, lda, B, ldb, bias, \
+                       alpha, o0, l0, o1, l1, aux, la, ep);                                    \
+    break;
+  switch (epi) {
+    LC_PP_CASE(EPI_BF16)
+    LC_PP_CASE(EPI_F32)
+    LC_PP_CASE(EPI_RESID)
+    LC_PP_CASE(EPI_GELU)
+    LC_PP_CASE(EPI_GELU_BWD)
+    LC_PP_CASE(EPI_BF16_F32)
+    LC_PP_CASE(EPI_AD_DOWN)
+    LC_PP_CASE(EPI_AD_UP)
+    LC_PP_CASE(EPI_AD_MASK)
+    LC_PP_CASE(EPI_AD_ADD)
+    default:
+      return LC_EINVAL;
+  }
+#undef LC_PP_CASE
+  LC_LAUNCH_RET();
+}
+
 // tile-shape selector (env LC_GEMM_TILE forces one for experiments: 0 auto, 1 = 128x128x2,
 // 2 = 256x128x3, 3 = 256x256x2, 4 = 128x64x2)
 int g_force_tile = -1;
+unsigned long long* g_dbg = nullptr;
 
 }  // namespace
 
@@ -438,13 +619,14 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   }
   int tile = g_force_tile;
   if (tile == 0) {
-    // measured on the ViT-B/16 step shapes (tools/bench_gemm.py): 256x256 for the wide
-    // N >= 2048 GEMMs, 128x128 at 2 workgroups/CU for N = 768 (better wave quantisation)
+    // measured on the ViT-B/16 step shapes (tools/bench_gemm.py): 256x256 ping-pong for the
+    // wide (N >= 2048) and deep (K >= 2048) GEMMs, 128x128 at 2 workgroups/CU otherwise
     if (N % 128 != 0) tile = 4;
-    else if (M >= 4096 && N % 256 == 0 && N >= 2048) tile = 3;
+    else if (M >= 4096 && N % 256 == 0 && (N >= 2048 || K >= 2048)) tile = 5;
     else tile = 1;
   }
-  if ((tile == 3 && N % 256) || ((tile == 1 || tile == 2) && N % 128)) tile = 4;
+  if (((tile == 3 || tile == 5 || tile == 6) && N % 256) || ((tile == 1 || tile == 2) && N % 128))
+    tile = 4;
   switch (tile) {
     case 1:
       return launch_nt<128, 128, 2, 2, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
@@ -455,6 +637,10 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     case 3:
       return launch_nt<256, 256, 2, 4, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                           ldo0, out1, ldo1, aux, ldaux, ep);
+    case 5:
+    case 6:
+      return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                       aux, ldaux, ep);
     default:
       return launch_nt<128, 64, 4, 1, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                          ldo0, out1, ldo1, aux, ldaux, ep);
@@ -468,13 +654,18 @@ int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, 
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux) {
   LC_CHECK_ARG(epi >= 0 && epi <= 5);
-  EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0};
+  EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
   return lc_gemm_nt_ex(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                        aux, ldaux, ep);
 }
 
+int lc_gemm_set_debug(unsigned long long* p) {
+  g_dbg = p;
+  return LC_OK;
+}
+
 int lc_gemm_set_tile(int tile) {
-  LC_CHECK_ARG(tile >= 0 && tile <= 4);
+  LC_CHECK_ARG(tile >= 0 && tile <= 6);
   g_force_tile = tile;
   return LC_OK;
 }

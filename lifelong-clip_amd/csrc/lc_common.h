@@ -77,6 +77,7 @@ struct EpiParams {
   float scale;       // adapter scalar
   float keep;        // 1 - dropout p
   uint64_t seed;     // dropout mask seed
+  unsigned long long* dbg;  // diagnostic timestamps (nullptr in production)
 };
 
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).

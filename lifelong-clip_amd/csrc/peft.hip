@@ -262,7 +262,7 @@ int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const 
                    unsigned long long seed, const float* resid, float* xout, long ldx, void* hout) {
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldz % 8 == 0 && ldx % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  EpiParams ep{z, ldz, scale, keep, (uint64_t)seed};
+  EpiParams ep{z, ldz, scale, keep, (uint64_t)seed, nullptr};
   int rc = lc_gemm_nt_ex(st, 6 /*EPI_AD_DOWN*/, M, AD_H, D, z, ldz, Wd, D, bd, 1.0f, hout, AD_H,
                          nullptr, 0, nullptr, 0, ep);
   if (rc) return rc;
@@ -277,7 +277,7 @@ int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, con
                    void* dz, long ldz) {
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  EpiParams ep{nullptr, 0, scale, keep, 0};
+  EpiParams ep{nullptr, 0, scale, keep, 0, nullptr};
   int rc = lc_gemm_nt_ex(st, 8 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
                          AD_H, nullptr, 0, h, AD_H, ep);
   if (rc) return rc;

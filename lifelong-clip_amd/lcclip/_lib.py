@@ -21,6 +21,7 @@ SIGNATURES = {
     "lc_gemm_nt": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_float, P, c_long, P,
                    c_long, P, c_long],
     "lc_gemm_set_tile": [c_int],
+    "lc_gemm_set_debug": [P],
     "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float],
     "lc_layernorm_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_int, c_long, P, P],
     "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
