@@ -6,7 +6,9 @@ batch 256 per GPU, 1x MI355X), on synthetic 224x224 images and C = 10 class prom
                   [--method adapter|lora] [--no-cpu-baseline]
 
 For N > 1 launch with torch.distributed.run (one process per GPU, RCCL); per-GPU work is fixed
-(weak scaling) and the only exchange is the all-reduce of the flat PEFT-gradient buffer.
+(weak scaling): images shard by rank, the C prompts are sharded across ranks (features
+all-gathered, dL/dT all-reduced), and the PEFT gradients are all-reduced in per-layer-group
+buckets overlapped with backward (lcclip/dp.py).
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -33,20 +35,22 @@ PEAK_BF16 = 2.5e15      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
 PEAK_HBM = 8.0e12
 
 
-def synthetic_batch(B, C, dev, seed):
+def synthetic_batch(B, C, dev, seed, tok_seed=7):
+    """Images / labels from `seed` (per rank); the C prompts from `tok_seed` (the same global
+    class list on every rank)."""
     g = torch.Generator(device=dev).manual_seed(seed)
     x = torch.rand(B, 3, 224, 224, device=dev, generator=g)
     mean = torch.tensor([0.5071, 0.4867, 0.4408], device=dev).view(1, 3, 1, 1)
     std = torch.tensor([0.2675, 0.2565, 0.2761], device=dev).view(1, 3, 1, 1)
     x = (x - mean) / std
-    gc = torch.Generator().manual_seed(seed + 7)
+    gc = torch.Generator().manual_seed(tok_seed)
     tok = torch.zeros(C, 77, dtype=torch.long)
     for i in range(C):
         k = int(torch.randint(6, 13, (1,), generator=gc))
         tok[i, 0] = 49406
         tok[i, 1:1 + k] = torch.randint(256, 49406, (k,), generator=gc)
         tok[i, 1 + k] = 49407
-    y = torch.randint(0, C, (B,), generator=gc)
+    y = torch.randint(0, C, (B,), generator=torch.Generator().manual_seed(seed))
     return x, tok.to(dev), y.to(dev)
 
 

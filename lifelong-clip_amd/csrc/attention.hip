@@ -6,68 +6,79 @@
 // Layout: qkv = [rows = batch*L, 3*D] bf16 (q | k | v, head h at columns h*64), as produced by
 // the fused QKV GEMM; O = [rows, D] bf16; lse = [batch*H, L] f32 (log2 domain).
 //
-// MI355X design: sequence lengths are short (197 image tokens, 77 text tokens), so one
-// workgroup owns one (image, head) pair and keeps the WHOLE key range on chip: K and V in LDS,
-// the full score row of 32 queries per wave in registers (no online-softmax rescaling). The
-// grid is batch*H workgroups (3072 at B=256). Keys are padded to Lp = 32*NQB; padded keys are
-// masked to -inf and padded V rows are zero.
-//   fwd: S^T = K Q^T (keys on the accumulator rows, queries on lanes), row max / sum across
-//        the 4 lane groups, P^T packed to bf16 straight from the accumulators into the
-//        B-operand of O^T = V^T P^T; V^T fragments come from ds_read_b64_tr_b16 (hardware
-//        transpose) of a row-major V image padded to 160-B rows (conflict-free tr reads).
-//   bwd: phase 1 — each wave owns 32 keys, sweeps all queries: S = Q K^T, dP = dO V^T,
-//        P = exp2(S*c - lse), dS = P (dP - D); dV^T += dO^T P and dK^T += Q^T dS with P / dS
-//        used directly as MFMA B-operands; dS^T is parked in LDS. phase 2 — each wave owns 32
-//        queries: dQ^T = K^T dS^T from transposed LDS reads. No atomics, no HBM round trip of
-//        S or P.
+// MI355X design. Sequences are short (197 image tokens, 77 text tokens): one workgroup owns one
+// (sequence, head) pair with the WHOLE key range on chip, one wave per 32 rows (queries or keys),
+// keys padded to Lp = 32*NQB (padded keys masked, padded rows zero). At d_head = 64 the
+// per-score work is dominated by VALU (scale, max, exp, sum, pack), not MFMA, so the kernels are
+// laid out to minimise VALU issue:
+//   * LDS images use a row swizzle that is invariant under 16-row steps, so every lane's LDS
+//     offsets are computed once; loop steps only add wave-uniform row-block offsets;
+//   * masking (padded keys, causal) runs only on the wave-uniform edge blocks, and causal blocks
+//     entirely above the diagonal are skipped;
+//   * fwd: EXACT softmax in two passes — pass 1 recomputes S^T = K Q^T only for the row max
+//     (MFMA is the idle pipe here), pass 2 forms p = exp2(S*c - m*c) with one FMA, packs P^T to
+//     bf16 straight from the accumulators into the B operand of O^T = V^T P^T (V^T via
+//     ds_read_b64_tr_b16); no online rescaling;
+//   * bwd, key-major kernel (dK, dV): each wave keeps its 32 keys' K / V fragments and dK^T, dV^T
+//     accumulators in registers and sweeps the queries: S = Q K^T, dP = dO V^T with -D preloaded
+//     as the dP accumulator, dS = P * dP, dV^T += dO^T P, dK^T += Q^T dS;
+//   * bwd, query-major kernel (dQ): each wave keeps its 32 queries' Q / dO fragments, recomputes
+//     S^T, dP^T from K / V in LDS and accumulates dQ^T = K^T dS^T; it walks the heads in reverse
+//     order so its reads hit what the key-major kernel left in L2 / the Infinity Cache.
 #include "lc_common.h"
 
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// raw v_exp_f32: arguments are <= 0 here, exp2(-inf) = 0, denormal results flush to 0
+LC_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+// padded key or (text tower) future key; bitwise ops keep it a select, not a branch
+LC_DEV bool masked(int key, int q, int L, int causal) {
+  return (key >= L) | ((causal != 0) & (key > q));
+}
+
+// 128-B-row images: 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7)
 LC_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-// 16 B fragment from a swizzled [rows][64 bf16] image (128 B rows)
-LC_DEV bf16x8 rd_row(const char* base, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(base + row * 128 + swz(row, chunk) * 16);
-}
-// transposed 4x16 read from the swizzled 128-B-row image; col multiple of 4
-LC_DEV bf16x4 tr_swz(const char* base, int row, int col) {
-  const int off = row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2;
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) bf16x4*)(base + off));
-}
-// transposed read from a plain image with a given row stride (bytes)
-LC_DEV bf16x4 tr_plain(const char* base, int stride, int row, int col) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) bf16x4*)(base + row * stride + col * 2));
+LC_DEV bf16x8 lds16(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+LC_DEV bf16x4 lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(p));
 }
 LC_DEV bf16x8 cat4(bf16x4 a, bf16x4 b) { return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+LC_DEV bf16x8 as_bf8(u32x4 v) { return __builtin_bit_cast(bf16x8, v); }
 LC_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
-  uint32_t w0 = pack2bf(a[0], a[1]), w1 = pack2bf(a[2], a[3]);
-  uint32_t w2 = pack2bf(b[0], b[1]), w3 = pack2bf(b[2], b[3]);
-  bf16x8 r;
-  r[0] = (short)(w0 & 0xffff); r[1] = (short)(w0 >> 16);
-  r[2] = (short)(w1 & 0xffff); r[3] = (short)(w1 >> 16);
-  r[4] = (short)(w2 & 0xffff); r[5] = (short)(w2 >> 16);
-  r[6] = (short)(w3 & 0xffff); r[7] = (short)(w3 >> 16);
-  return r;
+  return as_bf8(u32x4{pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])});
 }
 
 LC_DEV uint4 ld16_or_zero(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const uint4*>(p) : uint4{0, 0, 0, 0};
 }
 
-constexpr int V_STRIDE = 160;  // bytes per V row in LDS (conflict-free tr reads)
+// Lane offsets (bytes) into a swizzled 128-B-row image, valid for any row block that starts at a
+// multiple of 16 rows:
+//   row_off(t, g, s): A/B-operand read of row t (+block), k-chunk s*4+g  (16 B)
+//   tr_off(t, g, dt): transposed read of rows 4g + (t>>2) (+16 for the upper half), columns
+//                     dt*16 + (t&3)*4 .. +3 — the V^T / K^T / Q^T / dO^T fragment layout whose
+//                     k order matches a bf16x8 packed from two 16-row accumulator tiles.
+LC_DEV int row_off(int t, int g, int s) { return t * 128 + (((s * 4 + g) ^ ((t >> 1) & 7)) * 16); }
+LC_DEV int tr_off(int t, int g, int dt) {
+  const int row = 4 * g + (t >> 2);
+  const int col = dt * 16 + (t & 3) * 4;
+  return row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2;
+}
 
+constexpr int V_STRIDE = 160;  // bytes per V row in the forward's plain V image (conflict-free tr)
+
+// ----------------------------------------------------------------------------------- forward
 template <int NQB>
-__global__ void __launch_bounds__(64 * NQB)
+__global__ void __launch_bounds__(64 * NQB, 4)
 attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
                 bf16_t* __restrict__ O, long ldo, float* __restrict__ lse, int causal,
                 float scale) {
   constexpr int LP = 32 * NQB;
-  constexpr int NKT = 2 * NQB;
   constexpr int NTH = 64 * NQB;
   __shared__ __attribute__((aligned(16))) char smem[LP * 128 + LP * V_STRIDE];
   char* Ks = smem;
@@ -79,16 +90,17 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   const long base = (long)n * L;
   const float c = scale * LOG2E;
 
-  for (int idx = tid; idx < LP * 8; idx += NTH) {
-    const int r = idx >> 3, ch = idx & 7;
+  // staging: every lane issues all its 16-B loads before its first LDS write
+  constexpr int IT = LP * 8 / NTH;  // = 4
+  const int ch = tid & 7;
+  uint4 kv[IT], vv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
     const bf16_t* src = qkv + (base + r) * ldq + h * 64 + ch * 8;
-    const uint4 kv = ld16_or_zero(src + D, r < L);
-    const uint4 vv = ld16_or_zero(src + 2 * D, r < L);
-    *reinterpret_cast<uint4*>(Ks + r * 128 + swz(r, ch) * 16) = kv;
-    *reinterpret_cast<uint4*>(Vs + r * V_STRIDE + ch * 16) = vv;
+    kv[i] = ld16_or_zero(src + D, r < L);
+    vv[i] = ld16_or_zero(src + 2 * D, r < L);
   }
-
-  // Q fragments (B operand of S^T = K Q^T): Q[q][32s + 8g .. +7]
   const int qb = 32 * w;
   bf16x8 qf[2][2];
 #pragma unroll
@@ -100,66 +112,94 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
       qf[qt][s] = *reinterpret_cast<bf16x8*>(&u);
     }
   }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    *reinterpret_cast<uint4*>(Ks + r * 128 + swz(r, ch) * 16) = kv[i];
+    *reinterpret_cast<uint4*>(Vs + r * V_STRIDE + ch * 16) = vv[i];
+  }
   __syncthreads();
 
-  f32x4 S[NKT][2];
+  const char* k0 = Ks + row_off(t, g, 0);
+  const char* k1 = Ks + row_off(t, g, 1);
+  const char* vt = Vs + (4 * g + (t >> 2)) * V_STRIDE + (t & 3) * 8;
+  // key steps holding a key <= the wave's last query (causal) / < L
+  const int s_end = causal ? min(NQB, (qb + 31) / 32 + 1) : NQB;
+
+  // S^T tile pair of key step s: lane holds S^T[key = 32s + 16kk + 4g + r][q = qb + 16qt + t]
+  auto scores = [&](int s, f32x4 (&S)[2][2]) {
 #pragma unroll
-  for (int kt = 0; kt < NKT; ++kt) {
-    S[kt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    S[kt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ro = (32 * s + 16 * kk) * 128;
+      const bf16x8 ka = lds16(k0 + ro), kb = lds16(k1 + ro);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 kf = rd_row(Ks, kt * 16 + t, s * 4 + g);
-      S[kt][0] = mfma16(kf, qf[0][s], S[kt][0]);
-      S[kt][1] = mfma16(kf, qf[1][s], S[kt][1]);
+      for (int qt = 0; qt < 2; ++qt) {
+        S[kk][qt] = mfma16(ka, qf[qt][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S[kk][qt] = mfma16(kb, qf[qt][1], S[kk][qt]);
+      }
+    }
+    if (32 * s + 32 > L || (causal && 32 * s + 31 > qb)) {  // wave-uniform edge block
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            S[kk][qt][r] = masked(32 * s + 16 * kk + 4 * g + r, qb + 16 * qt + t, L, causal)
+                               ? -INFINITY : S[kk][qt][r];
+    }
+  };
+
+  // pass 1: exact row max of the raw scores
+  float mx[2] = {-INFINITY, -INFINITY};
+#pragma unroll 1
+  for (int s = 0; s < s_end; ++s) {
+    f32x4 S[2][2];
+    scores(s, S);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float m = mx[qt];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        m = fmaxf(fmaxf(m, fmaxf(S[kk][qt][0], S[kk][qt][1])), fmaxf(S[kk][qt][2], S[kk][qt][3]));
+      mx[qt] = m;
     }
   }
-  // lane holds S^T[key = kt*16 + 4g + r][q = qb + qt*16 + t]
-  float mx[2], sm[2];
+  float nm[2];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    const int q = qb + qt * 16 + t;
-    float m = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * 16 + 4 * g + r;
-        float v = S[kt][qt][r] * c;
-        if (key >= L || (causal && key > q)) v = -INFINITY;
-        S[kt][qt][r] = v;
-        m = fmaxf(m, v);
-      }
+    float m = mx[qt];
     m = fmaxf(m, __shfl_xor(m, 16));
     m = fmaxf(m, __shfl_xor(m, 32));
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(S[kt][qt][r] - m);
-        S[kt][qt][r] = p;
-        l += p;
-      }
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
-    mx[qt] = m;
-    sm[qt] = l;
+    mx[qt] = m * c;
+    nm[qt] = -m * c;
   }
 
+  // pass 2: P = exp2(S*c - m*c), row sums, O^T += V^T P^T
+  float sm[2] = {0.f, 0.f};
   f32x4 Oa[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) Oa[dt][0] = Oa[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int s = 0; s < s_end; ++s) {
+    f32x4 S[2][2];
+    scores(s, S);
 #pragma unroll
-  for (int s = 0; s < NQB; ++s) {
-    const bf16x8 pb0 = pack8(S[2 * s][0], S[2 * s + 1][0]);
-    const bf16x8 pb1 = pack8(S[2 * s][1], S[2 * s + 1][1]);
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = ex2(__builtin_fmaf(S[kk][qt][r], c, nm[qt]));
+          S[kk][qt][r] = p;
+          sm[qt] += p;
+        }
+    const bf16x8 pb0 = pack8(S[0][0], S[1][0]);
+    const bf16x8 pb1 = pack8(S[0][1], S[1][1]);
+    const char* vs = vt + 32 * s * V_STRIDE;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int col = dt * 16 + (t & 3) * 4;
-      const bf16x4 lo = tr_plain(Vs, V_STRIDE, 32 * s + 4 * g + (t >> 2), col);
-      const bf16x4 hi = tr_plain(Vs, V_STRIDE, 32 * s + 16 + 4 * g + (t >> 2), col);
-      const bf16x8 vf = cat4(lo, hi);
+      const bf16x8 vf = cat4(lds_tr(vs + dt * 32), lds_tr(vs + 16 * V_STRIDE + dt * 32));
       Oa[dt][0] = mfma16(vf, pb0, Oa[dt][0]);
       Oa[dt][1] = mfma16(vf, pb1, Oa[dt][1]);
     }
@@ -167,47 +207,37 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   // lane holds O^T[d = dt*16 + 4g + r][q = qb + qt*16 + t]
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
+    float l = sm[qt];
+    l += __shfl_xor(l, 16);
+    l += __shfl_xor(l, 32);
     const int q = qb + qt * 16 + t;
     if (q < L) {
-      const float inv = 1.0f / sm[qt];
+      const float inv = 1.0f / l;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const f32x4 o = Oa[dt][qt];
         *reinterpret_cast<uint2*>(O + (base + q) * ldo + h * 64 + dt * 16 + 4 * g) =
             uint2{pack2bf(o[0] * inv, o[1] * inv), pack2bf(o[2] * inv, o[3] * inv)};
       }
-      if (g == 0) lse[(long)nh * L + q] = mx[qt] + log2f(sm[qt]);
+      if (g == 0) lse[(long)nh * L + q] = mx[qt] + __log2f(l);
     }
   }
 }
 
-template <int NQB>
-struct BwdLds {
-  static constexpr int LP = 32 * NQB;
-  static constexpr int DST_STRIDE = LP * 2 + 16;  // bytes per dS^T row
-  static constexpr int Q_OFF = 0;
-  static constexpr int DO_OFF = LP * 128;
-  static constexpr int DST_OFF = 2 * LP * 128;
-  static constexpr int LSE_OFF = DST_OFF + LP * DST_STRIDE;
-  static constexpr int DQ_OFF = LSE_OFF + LP * 4;
-  static constexpr int BYTES = DQ_OFF + LP * 4;
-};
-
+// ------------------------------------------------------------------ backward, key-major (dK, dV)
 template <int NQB>
 __global__ void __launch_bounds__(64 * NQB)
-attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
-                const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
-                const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
-                float scale) {
-  using Lay = BwdLds<NQB>;
-  constexpr int LP = Lay::LP;
+attn_bwd_kv_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
+                   const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
+                   const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
+                   float scale) {
+  constexpr int LP = 32 * NQB;
   constexpr int NTH = 64 * NQB;
-  __shared__ __attribute__((aligned(16))) char smem[Lay::BYTES];
-  char* Qs = smem + Lay::Q_OFF;
-  char* dOs = smem + Lay::DO_OFF;
-  char* dSTs = smem + Lay::DST_OFF;
-  float* lse_s = reinterpret_cast<float*>(smem + Lay::LSE_OFF);
-  float* dq_s = reinterpret_cast<float*>(smem + Lay::DQ_OFF);
+  __shared__ __attribute__((aligned(16))) char smem[2 * LP * 128 + 2 * LP * 4];
+  char* Qs = smem;
+  char* dOs = smem + LP * 128;
+  float* nlse_s = reinterpret_cast<float*>(smem + 2 * LP * 128);  // -lse
+  float* nd_s = nlse_s + LP;                                       // -D
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, t = lane & 15;
@@ -215,33 +245,21 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   const long base = (long)n * L;
   const float c = scale * LOG2E;
 
-  for (int idx = tid; idx < LP * 8; idx += NTH) {
-    const int r = idx >> 3, ch = idx & 7;
-    const uint4 qv = ld16_or_zero(qkv + (base + r) * ldq + h * 64 + ch * 8, r < L);
-    const uint4 dv = ld16_or_zero(dO + (base + r) * ldo + h * 64 + ch * 8, r < L);
-    *reinterpret_cast<uint4*>(Qs + r * 128 + swz(r, ch) * 16) = qv;
-    *reinterpret_cast<uint4*>(dOs + r * 128 + swz(r, ch) * 16) = dv;
-  }
-  for (int q = tid; q < LP; q += NTH) {
-    float dsum = 0.f, lv = 1e30f;
-    if (q < L) {
-      const bf16_t* po = O + (base + q) * ldo + h * 64;
-      const bf16_t* pd = dO + (base + q) * ldo + h * 64;
+  // staging: all 16-B loads of Q, dO and O issued before the first LDS write; D = rowsum(dO*O)
+  // from the same chunks (8 lanes per row, reduced with xor-shuffles)
+  constexpr int IT = LP * 8 / NTH;  // = 4
+  const int ch = tid & 7;
+  uint4 qv[IT], dv[IT], ov[IT];
+  float lv[IT];
 #pragma unroll
-      for (int ch = 0; ch < 8; ++ch) {
-        const uint4 a = *reinterpret_cast<const uint4*>(po + ch * 8);
-        const uint4 b = *reinterpret_cast<const uint4*>(pd + ch * 8);
-        const uint32_t aa[4] = {a.x, a.y, a.z, a.w}, bb[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          dsum += bf2f(aa[k] & 0xffff) * bf2f(bb[k] & 0xffff) + bf2f(aa[k] >> 16) * bf2f(bb[k] >> 16);
-      }
-      lv = lse[(long)nh * L + q];
-    }
-    dq_s[q] = dsum;
-    lse_s[q] = lv;
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    const long off = h * 64 + ch * 8;
+    qv[i] = ld16_or_zero(qkv + (base + r) * ldq + off, r < L);
+    dv[i] = ld16_or_zero(dO + (base + r) * ldo + off, r < L);
+    ov[i] = ld16_or_zero(O + (base + r) * ldo + off, r < L);
+    lv[i] = (r < L) ? lse[(long)nh * L + r] : 1e30f;
   }
-
   // own key block: K / V rows kb + kt2*16 + t, as B-operand fragments
   const int kb = 32 * w;
   bf16x8 kf[2][2], vf[2][2];
@@ -256,7 +274,30 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
       vf[kt2][s] = *reinterpret_cast<bf16x8*>(&vu);
     }
   }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    *reinterpret_cast<uint4*>(Qs + r * 128 + swz(r, ch) * 16) = qv[i];
+    *reinterpret_cast<uint4*>(dOs + r * 128 + swz(r, ch) * 16) = dv[i];
+    const uint32_t aa[4] = {ov[i].x, ov[i].y, ov[i].z, ov[i].w};
+    const uint32_t bb[4] = {dv[i].x, dv[i].y, dv[i].z, dv[i].w};
+    float dsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      dsum += bf2f(aa[k] & 0xffff) * bf2f(bb[k] & 0xffff) + bf2f(aa[k] >> 16) * bf2f(bb[k] >> 16);
+    dsum += __shfl_xor(dsum, 1);
+    dsum += __shfl_xor(dsum, 2);
+    dsum += __shfl_xor(dsum, 4);
+    if (ch == 0) {
+      nd_s[r] = -dsum;
+      nlse_s[r] = -lv[i];
+    }
+  }
   __syncthreads();
+
+  const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
+  const int tr0 = tr_off(t, g, 0), tr1 = tr_off(t, g, 1), tr2 = tr_off(t, g, 2), tr3 = tr_off(t, g, 3);
+  const int tro[4] = {tr0, tr1, tr2, tr3};
 
   f32x4 dV[4][2], dK[4][2];
 #pragma unroll
@@ -264,68 +305,235 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) dV[dt][k2] = dK[dt][k2] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int qc = 0; qc < NQB; ++qc) {
-    f32x4 S[2][2], dP[2][2];
+  // causal: queries before the block's first key see none of its keys
+  const int qc0 = causal ? w : 0;
+#pragma unroll 1
+  for (int qc = qc0; qc < NQB; ++qc) {
+    const bool edge = (kb + 32 > L) || (causal && kb + 31 > qc * 32);
+    // B operands (k = 32 queries of this chunk): slot j<4 -> q = 4g+j, j>=4 -> 16+4g+(j-4);
+    // one 16-query tile of S / dP is live at a time and packed to bf16 straight away.
+    u32x4 pw[2], sw[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
+      const int q0 = qc * 32 + qt * 16 + 4 * g;
+      const f32x4 nl = *reinterpret_cast<const f32x4*>(nlse_s + q0);
+      const f32x4 nd = *reinterpret_cast<const f32x4*>(nd_s + q0);
+      const char* qrow = Qs + (qc * 32 + qt * 16) * 128;
+      const char* drow = dOs + (qc * 32 + qt * 16) * 128;
+      const bf16x8 qa0 = lds16(qrow + ro0), qa1 = lds16(qrow + ro1);
+      const bf16x8 da0 = lds16(drow + ro0), da1 = lds16(drow + ro1);
+      f32x4 S[2], dP[2];
 #pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) S[qt][k2] = dP[qt][k2] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k2 = 0; k2 < 2; ++k2) {
+        S[k2] = mfma16(qa0, kf[k2][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S[k2] = mfma16(qa1, kf[k2][1], S[k2]);
+        dP[k2] = mfma16(da0, vf[k2][0], nd);  // dP - D
+        dP[k2] = mfma16(da1, vf[k2][1], dP[k2]);
+      }
+      // lane holds X[q = q0 + r][key = kb + k2*16 + t]
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int row = qc * 32 + qt * 16 + t;
-        const bf16x8 qa = rd_row(Qs, row, s * 4 + g);
-        const bf16x8 da = rd_row(dOs, row, s * 4 + g);
+      for (int k2 = 0; k2 < 2; ++k2) {
+        f32x4 p;
 #pragma unroll
-        for (int k2 = 0; k2 < 2; ++k2) {
-          S[qt][k2] = mfma16(qa, kf[k2][s], S[qt][k2]);
-          dP[qt][k2] = mfma16(da, vf[k2][s], dP[qt][k2]);
+        for (int r = 0; r < 4; ++r) p[r] = ex2(__builtin_fmaf(S[k2][r], c, nl[r]));
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[r] = masked(kb + k2 * 16 + t, q0 + r, L, causal) ? 0.f : p[r];
         }
+        const f32x4 ds = p * dP[k2];
+        pw[k2][2 * qt] = pack2bf(p[0], p[1]);
+        pw[k2][2 * qt + 1] = pack2bf(p[2], p[3]);
+        sw[k2][2 * qt] = pack2bf(ds[0], ds[1]);
+        sw[k2][2 * qt + 1] = pack2bf(ds[2], ds[3]);
       }
     }
-    // lane holds X[q = qc*32 + qt*16 + 4g + r][key = kb + k2*16 + t]
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = qc * 32 + qt * 16 + 4 * g + r;
-          const int key = kb + k2 * 16 + t;
-          float p = exp2f(S[qt][k2][r] * c - lse_s[q]);
-          if (key >= L || (causal && key > q)) p = 0.f;
-          S[qt][k2][r] = p;
-          dP[qt][k2][r] = p * (dP[qt][k2][r] - dq_s[q]);
-        }
-    // B operands (k = 32 queries of this chunk): slot j<4 -> q = 4g+j, j>=4 -> 16+4g+(j-4)
-    bf16x8 pB[2], sB[2];
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      pB[k2] = pack8(S[0][k2], S[1][k2]);
-      sB[k2] = pack8(dP[0][k2], dP[1][k2]);
-    }
+    const bf16x8 pB[2] = {as_bf8(pw[0]), as_bf8(pw[1])};
+    const bf16x8 sB[2] = {as_bf8(sw[0]), as_bf8(sw[1])};
+    const char* qblk = Qs + qc * 32 * 128;
+    const char* dblk = dOs + qc * 32 * 128;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int col = dt * 16 + (t & 3) * 4;
-      const int r0 = qc * 32 + 4 * g + (t >> 2);
-      const bf16x8 doT = cat4(tr_swz(dOs, r0, col), tr_swz(dOs, r0 + 16, col));
-      const bf16x8 qT = cat4(tr_swz(Qs, r0, col), tr_swz(Qs, r0 + 16, col));
+      const bf16x8 doT = cat4(lds_tr(dblk + tro[dt]), lds_tr(dblk + 16 * 128 + tro[dt]));
+      const bf16x8 qT = cat4(lds_tr(qblk + tro[dt]), lds_tr(qblk + 16 * 128 + tro[dt]));
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
         dV[dt][k2] = mfma16(doT, pB[k2], dV[dt][k2]);
         dK[dt][k2] = mfma16(qT, sB[k2], dK[dt][k2]);
       }
     }
-    // park dS^T[key][q]: 4 consecutive q per lane -> one 8-B LDS store
+  }
+  // dK, dV of the own key block: lane holds X^T[d = dt*16 + 4g + r][key = kb + k2*16 + t]
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+  for (int k2 = 0; k2 < 2; ++k2) {
+    const int key = kb + k2 * 16 + t;
+    if (key < L) {
+      bf16_t* dst = dqkv + (base + key) * lddq + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x4 a = dK[dt][k2], b = dV[dt][k2];
+        *reinterpret_cast<uint2*>(dst + D + dt * 16 + 4 * g) =
+            uint2{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale)};
+        *reinterpret_cast<uint2*>(dst + 2 * D + dt * 16 + 4 * g) =
+            uint2{pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- backward, fused (dK, dV, then dQ)
+template <int NQB>
+struct BwdLds {
+  static constexpr int LP = 32 * NQB;
+  static constexpr int DST_STRIDE = LP * 2 + 16;  // bytes per dS^T row (conflict-free tr reads)
+  static constexpr int Q_OFF = 0;
+  static constexpr int DO_OFF = LP * 128;
+  static constexpr int DST_OFF = 2 * LP * 128;
+  static constexpr int NLSE_OFF = DST_OFF + LP * DST_STRIDE;
+  static constexpr int ND_OFF = NLSE_OFF + LP * 4;
+  static constexpr int BYTES = ND_OFF + LP * 4;
+};
+
+template <int NQB>
+__global__ void __launch_bounds__(64 * NQB)
+attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
+                   const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
+                   const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
+                   float scale) {
+  constexpr int LP = 32 * NQB;
+  constexpr int NTH = 64 * NQB;
+  using Lay = BwdLds<NQB>;
+  __shared__ __attribute__((aligned(16))) char smem[Lay::BYTES];
+  char* Qs = smem + Lay::Q_OFF;
+  char* dOs = smem + Lay::DO_OFF;
+  char* dSTs = smem + Lay::DST_OFF;
+  float* nlse_s = reinterpret_cast<float*>(smem + Lay::NLSE_OFF);  // -lse
+  float* nd_s = reinterpret_cast<float*>(smem + Lay::ND_OFF);      // -D
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, t = lane & 15;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const long base = (long)n * L;
+  const float c = scale * LOG2E;
+
+  // staging: all 16-B loads of Q, dO and O issued before the first LDS write; D = rowsum(dO*O)
+  // from the same chunks (8 lanes per row, reduced with xor-shuffles)
+  constexpr int IT = LP * 8 / NTH;  // = 4
+  const int ch = tid & 7;
+  uint4 qv[IT], dv[IT], ov[IT];
+  float lv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    const long off = h * 64 + ch * 8;
+    qv[i] = ld16_or_zero(qkv + (base + r) * ldq + off, r < L);
+    dv[i] = ld16_or_zero(dO + (base + r) * ldo + off, r < L);
+    ov[i] = ld16_or_zero(O + (base + r) * ldo + off, r < L);
+    lv[i] = (r < L) ? lse[(long)nh * L + r] : 1e30f;
+  }
+  // own key block: K / V rows kb + kt2*16 + t, as B-operand fragments
+  const int kb = 32 * w;
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int kt2 = 0; kt2 < 2; ++kt2) {
+    const int key = kb + kt2 * 16 + t;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16_t* src = qkv + (base + key) * ldq + h * 64 + s * 32 + g * 8;
+      uint4 ku = ld16_or_zero(src + D, key < L), vu = ld16_or_zero(src + 2 * D, key < L);
+      kf[kt2][s] = *reinterpret_cast<bf16x8*>(&ku);
+      vf[kt2][s] = *reinterpret_cast<bf16x8*>(&vu);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    *reinterpret_cast<uint4*>(Qs + r * 128 + swz(r, ch) * 16) = qv[i];
+    *reinterpret_cast<uint4*>(dOs + r * 128 + swz(r, ch) * 16) = dv[i];
+    const uint32_t aa[4] = {ov[i].x, ov[i].y, ov[i].z, ov[i].w};
+    const uint32_t bb[4] = {dv[i].x, dv[i].y, dv[i].z, dv[i].w};
+    float dsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      dsum += bf2f(aa[k] & 0xffff) * bf2f(bb[k] & 0xffff) + bf2f(aa[k] >> 16) * bf2f(bb[k] >> 16);
+    dsum += __shfl_xor(dsum, 1);
+    dsum += __shfl_xor(dsum, 2);
+    dsum += __shfl_xor(dsum, 4);
+    if (ch == 0) {
+      nd_s[r] = -dsum;
+      nlse_s[r] = -lv[i];
+    }
+  }
+  __syncthreads();
+
+  const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
+  const int tr0 = tr_off(t, g, 0), tr1 = tr_off(t, g, 1), tr2 = tr_off(t, g, 2), tr3 = tr_off(t, g, 3);
+  const int tro[4] = {tr0, tr1, tr2, tr3};
+
+  f32x4 dV[4][2], dK[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) dV[dt][k2] = dK[dt][k2] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // causal: queries before the block's first key see none of its keys
+  const int qc0 = causal ? w : 0;
+#pragma unroll 1
+  for (int qc = qc0; qc < NQB; ++qc) {
+    const bool edge = (kb + 32 > L) || (causal && kb + 31 > qc * 32);
+    // B operands (k = 32 queries of this chunk): slot j<4 -> q = 4g+j, j>=4 -> 16+4g+(j-4);
+    // one 16-query tile of S / dP is live at a time and packed to bf16 straight away.
+    u32x4 pw[2], sw[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q0 = qc * 32 + qt * 16 + 4 * g;
+      const f32x4 nl = *reinterpret_cast<const f32x4*>(nlse_s + q0);
+      const f32x4 nd = *reinterpret_cast<const f32x4*>(nd_s + q0);
+      const char* qrow = Qs + (qc * 32 + qt * 16) * 128;
+      const char* drow = dOs + (qc * 32 + qt * 16) * 128;
+      const bf16x8 qa0 = lds16(qrow + ro0), qa1 = lds16(qrow + ro1);
+      const bf16x8 da0 = lds16(drow + ro0), da1 = lds16(drow + ro1);
+      f32x4 S[2], dP[2];
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
-        const int key = kb + k2 * 16 + t;
-        const int q0 = qc * 32 + qt * 16 + 4 * g;
-        const f32x4 v = dP[qt][k2];
-        *reinterpret_cast<uint2*>(dSTs + key * Lay::DST_STRIDE + q0 * 2) =
-            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        S[k2] = mfma16(qa0, kf[k2][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S[k2] = mfma16(qa1, kf[k2][1], S[k2]);
+        dP[k2] = mfma16(da0, vf[k2][0], nd);  // dP - D
+        dP[k2] = mfma16(da1, vf[k2][1], dP[k2]);
       }
+      // lane holds X[q = q0 + r][key = kb + k2*16 + t]
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        f32x4 p;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = ex2(__builtin_fmaf(S[k2][r], c, nl[r]));
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[r] = masked(kb + k2 * 16 + t, q0 + r, L, causal) ? 0.f : p[r];
+        }
+        const f32x4 ds = p * dP[k2];
+        pw[k2][2 * qt] = pack2bf(p[0], p[1]);
+        pw[k2][2 * qt + 1] = pack2bf(p[2], p[3]);
+        sw[k2][2 * qt] = pack2bf(ds[0], ds[1]);
+        sw[k2][2 * qt + 1] = pack2bf(ds[2], ds[3]);
+        // park dS^T[key][q0..q0+3] for the dQ phase
+        *reinterpret_cast<uint2*>(dSTs + (kb + k2 * 16 + t) * Lay::DST_STRIDE + q0 * 2) =
+            uint2{sw[k2][2 * qt], sw[k2][2 * qt + 1]};
+      }
+    }
+    const bf16x8 pB[2] = {as_bf8(pw[0]), as_bf8(pw[1])};
+    const bf16x8 sB[2] = {as_bf8(sw[0]), as_bf8(sw[1])};
+    const char* qblk = Qs + qc * 32 * 128;
+    const char* dblk = dOs + qc * 32 * 128;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 doT = cat4(lds_tr(dblk + tro[dt]), lds_tr(dblk + 16 * 128 + tro[dt]));
+      const bf16x8 qT = cat4(lds_tr(qblk + tro[dt]), lds_tr(qblk + 16 * 128 + tro[dt]));
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        dV[dt][k2] = mfma16(doT, pB[k2], dV[dt][k2]);
+        dK[dt][k2] = mfma16(qT, sB[k2], dK[dt][k2]);
+      }
+    }
   }
   // dK, dV of the own key block: lane holds X^T[d = dt*16 + 4g + r][key = kb + k2*16 + t]
 #pragma unroll
@@ -354,27 +562,165 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
     }
   __syncthreads();
 
-  // phase 2: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for queries qb..qb+31
+  // phase 2: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for queries qb..qb+31 (k order:
+  // key = 32s + 8g + j, from rows 8g+(t>>2) and 8g+4+(t>>2) of both images)
   const int qb = 32 * w;
+  const int s_end = causal ? min(NQB, w + 1) : NQB;
+  int klo[4], khi[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int col = dt * 16 + (t & 3) * 4;
+    const int r0 = 8 * g + (t >> 2);
+    klo[dt] = r0 * 128 + swz(r0, col >> 3) * 16 + (col & 7) * 2;
+    khi[dt] = (r0 + 4) * 128 + swz(r0 + 4, col >> 3) * 16 + (col & 7) * 2;
+  }
+  const char* dst0 = dSTs + (8 * g + (t >> 2)) * Lay::DST_STRIDE + (qb + (t & 3) * 4) * 2;
   f32x4 dQ[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) dQ[dt][0] = dQ[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < NQB; ++s) {
-    const int r0 = s * 32 + 8 * g + (t >> 2);
-    bf16x8 bq[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const int col = qb + qt * 16 + (t & 3) * 4;
-      bq[qt] = cat4(tr_plain(dSTs, Lay::DST_STRIDE, r0, col), tr_plain(dSTs, Lay::DST_STRIDE, r0 + 4, col));
-    }
+#pragma unroll 1
+  for (int s = 0; s < s_end; ++s) {
+    const char* ds = dst0 + 32 * s * Lay::DST_STRIDE;
+    const bf16x8 bq0 = cat4(lds_tr(ds), lds_tr(ds + 4 * Lay::DST_STRIDE));
+    const bf16x8 bq1 = cat4(lds_tr(ds + 32), lds_tr(ds + 4 * Lay::DST_STRIDE + 32));
+    const char* kblk = Ks + 32 * s * 128;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      const int col = dt * 16 + (t & 3) * 4;
-      const bf16x8 ka = cat4(tr_swz(Ks, r0, col), tr_swz(Ks, r0 + 4, col));
-      dQ[dt][0] = mfma16(ka, bq[0], dQ[dt][0]);
-      dQ[dt][1] = mfma16(ka, bq[1], dQ[dt][1]);
+      const bf16x8 ka = cat4(lds_tr(kblk + klo[dt]), lds_tr(kblk + khi[dt]));
+      dQ[dt][0] = mfma16(ka, bq0, dQ[dt][0]);
+      dQ[dt][1] = mfma16(ka, bq1, dQ[dt][1]);
     }
   }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qb + qt * 16 + t;
+    if (q < L) {
+      bf16_t* dst = dqkv + (base + q) * lddq + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const f32x4 a = dQ[dt][qt];
+        *reinterpret_cast<uint2*>(dst + dt * 16 + 4 * g) =
+            uint2{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale)};
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward, query-major (dQ)
+template <int NQB>
+__global__ void __launch_bounds__(64 * NQB, 4)
+attn_bwd_q_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
+                  const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
+                  const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
+                  float scale) {
+  constexpr int LP = 32 * NQB;
+  constexpr int NTH = 64 * NQB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * LP * 128];
+  char* Ks = smem;
+  char* Vs = smem + LP * 128;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, t = lane & 15;
+  // reverse order: the key-major kernel touched the last heads most recently (L2 / Infinity Cache)
+  const int nh = gridDim.x - 1 - blockIdx.x, n = nh / H, h = nh % H;
+  const long base = (long)n * L;
+  const float c = scale * LOG2E;
+
+  constexpr int IT = LP * 8 / NTH;  // = 4
+  const int ch = tid & 7;
+  uint4 kv[IT], vv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    const bf16_t* src = qkv + (base + r) * ldq + h * 64 + ch * 8;
+    kv[i] = ld16_or_zero(src + D, r < L);
+    vv[i] = ld16_or_zero(src + 2 * D, r < L);
+  }
+  const int qb = 32 * w;
+  bf16x8 qf[2][2], df[2][2];
+  float nl[2], nd[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int q = qb + qt * 16 + t;
+    float dsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const long off = h * 64 + s * 32 + g * 8;
+      uint4 u = ld16_or_zero(qkv + (base + q) * ldq + off, q < L);
+      uint4 d = ld16_or_zero(dO + (base + q) * ldo + off, q < L);
+      uint4 o = ld16_or_zero(O + (base + q) * ldo + off, q < L);
+      qf[qt][s] = *reinterpret_cast<bf16x8*>(&u);
+      df[qt][s] = *reinterpret_cast<bf16x8*>(&d);
+      const uint32_t oo[4] = {o.x, o.y, o.z, o.w}, dd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        dsum += bf2f(oo[k] & 0xffff) * bf2f(dd[k] & 0xffff) + bf2f(oo[k] >> 16) * bf2f(dd[k] >> 16);
+    }
+    dsum += __shfl_xor(dsum, 16);
+    dsum += __shfl_xor(dsum, 32);
+    nd[qt] = -dsum;
+    nl[qt] = q < L ? -lse[(long)nh * L + q] : -1e30f;
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    *reinterpret_cast<uint4*>(Ks + r * 128 + swz(r, ch) * 16) = kv[i];
+    *reinterpret_cast<uint4*>(Vs + r * 128 + swz(r, ch) * 16) = vv[i];
+  }
+  __syncthreads();
+
+  const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
+  const int tro[4] = {tr_off(t, g, 0), tr_off(t, g, 1), tr_off(t, g, 2), tr_off(t, g, 3)};
+  const int s_end = causal ? min(NQB, (qb + 31) / 32 + 1) : NQB;
+
+  f32x4 dQ[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dQ[dt][0] = dQ[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int s = 0; s < s_end; ++s) {
+    const bool edge = (32 * s + 32 > L) || (causal && 32 * s + 31 > qb);
+    // one 16-key tile of S^T / dP^T live at a time, packed to bf16 straight away
+    u32x4 sw[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ro = (32 * s + 16 * kk) * 128;
+      const bf16x8 ka0 = lds16(Ks + ro + ro0), ka1 = lds16(Ks + ro + ro1);
+      const bf16x8 va0 = lds16(Vs + ro + ro0), va1 = lds16(Vs + ro + ro1);
+      f32x4 S[2], dP[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        S[qt] = mfma16(ka0, qf[qt][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S[qt] = mfma16(ka1, qf[qt][1], S[qt]);
+        dP[qt] = mfma16(va0, df[qt][0], f32x4{nd[qt], nd[qt], nd[qt], nd[qt]});
+        dP[qt] = mfma16(va1, df[qt][1], dP[qt]);
+      }
+      // lane holds X^T[key = 32s + 16kk + 4g + r][q = qb + qt*16 + t]
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f32x4 p;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = ex2(__builtin_fmaf(S[qt][r], c, nl[qt]));
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            p[r] = masked(32 * s + 16 * kk + 4 * g + r, qb + qt * 16 + t, L, causal) ? 0.f : p[r];
+        }
+        const f32x4 ds = p * dP[qt];
+        sw[qt][2 * kk] = pack2bf(ds[0], ds[1]);
+        sw[qt][2 * kk + 1] = pack2bf(ds[2], ds[3]);
+      }
+    }
+    const bf16x8 sb0 = as_bf8(sw[0]);
+    const bf16x8 sb1 = as_bf8(sw[1]);
+    const char* kblk = Ks + 32 * s * 128;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 kT = cat4(lds_tr(kblk + tro[dt]), lds_tr(kblk + 16 * 128 + tro[dt]));
+      dQ[dt][0] = mfma16(kT, sb0, dQ[dt][0]);
+      dQ[dt][1] = mfma16(kT, sb1, dQ[dt][1]);
+    }
+  }
+  // lane holds dQ^T[d = dt*16 + 4g + r][q = qb + qt*16 + t]
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = qb + qt * 16 + t;
@@ -418,18 +764,43 @@ int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
 
 int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long ldq, const void* O,
                 const void* dO, long ldo, const float* lse, void* dqkv, long lddq, int causal) {
-  LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 224 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
+  LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 256 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
   LC_CHECK_ARG(lddq >= 3 * H * 64 && ldq % 8 == 0 && ldo % 8 == 0 && lddq % 8 == 0);
   const int D = H * 64;
   const int nqb = (L + 31) / 32;
   dim3 grid(n_seq * H);
   const float scale = 0.125f;
+  // fused single-pass kernel (dS^T parked in LDS, 1 workgroup per CU) up to 224 keys; the split
+  // key-major + query-major pair beyond that (LDS) or when LC_ATTN_BWD_SPLIT=1
+  static const int force_split = [] {
+    const char* e = getenv("LC_ATTN_BWD_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  const bool split = force_split != 0;
+  if (nqb == 8) {
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<8>, grid, dim3(512), 0, st, L, H, D, (const bf16_t*)qkv,
+                       ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, (bf16_t*)dqkv, lddq,
+                       causal, scale);
+    hipLaunchKernelGGL(attn_bwd_q_kernel<8>, grid, dim3(512), 0, st, L, H, D, (const bf16_t*)qkv,
+                       ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, (bf16_t*)dqkv, lddq,
+                       causal, scale);
+    LC_LAUNCH_RET();
+  }
   switch (nqb) {
 #define LC_AB(Q)                                                                                \
   case Q:                                                                                      \
-    hipLaunchKernelGGL(attn_bwd_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,                 \
-                       (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, \
-                       (bf16_t*)dqkv, lddq, causal, scale);                                    \
+    if (split)                                                                                 \
+      hipLaunchKernelGGL(attn_bwd_kv_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,            \
+                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
+                         lse, (bf16_t*)dqkv, lddq, causal, scale);                             \
+    if (split)                                                                                 \
+      hipLaunchKernelGGL(attn_bwd_q_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,             \
+                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
+                         lse, (bf16_t*)dqkv, lddq, causal, scale);                             \
+    else                                                                                       \
+      hipLaunchKernelGGL(attn_bwd_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,               \
+                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
+                         lse, (bf16_t*)dqkv, lddq, causal, scale);                             \
     break;
     LC_AB(1) LC_AB(2) LC_AB(3) LC_AB(4) LC_AB(5) LC_AB(6) LC_AB(7)
 #undef LC_AB

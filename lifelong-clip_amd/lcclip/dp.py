@@ -1,0 +1,93 @@
+"""Data-parallel exchange of the online step, one process per GPU.
+
+The reference replicates the model with nn.DataParallel and computes ONE loss over the gathered
+global batch (methods/adapter_clip.py:84-89, _trainer.py:168); the backbone is frozen, the loss
+is per-image CE over class logits, so images shard along the batch with no data-path collective.
+What remains is:
+
+  * PEFT gradients: averaged over ranks. They live in one flat fp32 buffer; per-layer-group
+    buckets are all-reduced asynchronously as soon as backward has finished those layers, so
+    the exchange overlaps the rest of backward (RCCL runs on its own stream; on gloo the same
+    calls run on the CPU for the tests). SUM on the wire, one 1/world scale at the end (gloo has
+    no AVG).
+  * text prompts: every rank needs the features of ALL C prompts (the logit columns), but the
+    text tower is not replicated: rank r encodes prompts [r*per, (r+1)*per) (the list padded to
+    per*world by repeating the last prompt), the feature rows are all-gathered, and dL/dT from
+    every rank's images is all-reduced (SUM) before each rank backpropagates its own slice.
+    Because dT is summed, a rank's text gradients come out world x its slice's share; the final
+    1/world scale of the flat buffer then leaves exactly the sum of the slices — the gradient of
+    the global-mean loss.
+  * labels / class list: every rank passes the GLOBAL batch labels to remap_labels so the logit
+    columns agree (the reference MVP trainer all-gathers them, methods/mvp_clip.py:305-313).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class DataParallel:
+    """Rank bookkeeping + the three exchanges. world == 1 makes every call a no-op."""
+
+    def __init__(self, group=None, enabled=None):
+        on = dist.is_available() and dist.is_initialized()
+        self.enabled = on if enabled is None else (enabled and on)
+        self.group = group
+        self.world = dist.get_world_size(group) if self.enabled else 1
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        self._works = []
+
+    # ---------------------------------------------------------------- prompt sharding
+    def prompt_slice(self, C: int):
+        """(lo, hi, per): this rank's rows of the padded prompt list."""
+        per = -(-C // self.world)
+        lo = self.rank * per
+        return lo, lo + per, per
+
+    def shard_tokens(self, tokens):
+        C = tokens.shape[0]
+        lo, hi, per = self.prompt_slice(C)
+        pad = per * self.world - C
+        if pad:
+            tokens = torch.cat([tokens, tokens[-1:].expand(pad, -1)], 0)
+        return tokens[lo:hi].contiguous()
+
+    def gather_rows(self, rows, C: int):
+        """All-gather the per-rank [per, E] feature slices into [C, E] (padding dropped)."""
+        if self.world == 1:
+            return rows[:C]
+        parts = [torch.empty_like(rows) for _ in range(self.world)]
+        dist.all_gather(parts, rows.contiguous(), group=self.group)
+        return torch.cat(parts, 0)[:C]
+
+    def sum_async(self, t):
+        """Asynchronous in-place SUM all-reduce; returns a handle with .wait() (or None)."""
+        if self.world == 1:
+            return None
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    # ---------------------------------------------------------------- gradient buckets
+    def launch_bucket(self, flat, lo: int, hi: int):
+        if self.world > 1 and hi > lo:
+            self._works.append(self.sum_async(flat[lo:hi]))
+
+    def finish_buckets(self, flat):
+        """Wait for every bucket and turn the sums into means."""
+        if self.world == 1:
+            return
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+        flat.mul_(1.0 / self.world)
+
+
+def layer_ranges(stack, base: int = 0):
+    """[(lo, hi)] offsets of each block's PEFT parameters inside a flat buffer whose layout is
+    stack.trainable_params() in order, starting at `base`."""
+    out = []
+    off = base
+    for b in stack.blocks:
+        n = sum(p.numel() for p in b.peft_parameters())
+        out.append((off, off + n))
+        off += n
+    return out

@@ -181,9 +181,10 @@ class BlockStack:
         return x, saved
 
     # ------------------------------------------------------------------ backward
-    def backward(self, saved, dx, dxb, grads, n_seq: int, L: int):
+    def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
-        param -> f32 tensor (accumulated). Returns (dx, dxb) w.r.t. the stack input."""
+        param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
+        have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input."""
         M, D = dx.shape
         H = self.n_head
         dev = dx.device
@@ -224,6 +225,8 @@ class BlockStack:
                                 attn.in_proj_weight_lora_B, attn.scaling, grads)
             ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
                               dxb_new, dres=dx_mid)
+            if on_layer is not None:
+                on_layer(li)
             # ping-pong: the consumed output-gradient buffers are recycled for the next layer
             dx, dx_new = dx_new, dx
             dxb, dxb_new = dxb_new, dxb
@@ -304,7 +307,7 @@ class ImageTower:
         ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads):
+    def backward(self, ctx, df, grads, on_layer=None):
         v = self.visual
         dev = df.device
         n, L = ctx["n"], ctx["L"]
@@ -317,7 +320,7 @@ class ImageTower:
         dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L)
+        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer)
 
 
 class TextTower:
@@ -360,7 +363,7 @@ class TextTower:
         ctx = dict(saved=saved, x=x, eot=eot, mean=mean, rstd=rstd, C=C, L=L) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads):
+    def backward(self, ctx, df, grads, on_layer=None):
         c = self.clip
         dev = df.device
         C, L = ctx["C"], ctx["L"]
@@ -373,4 +376,4 @@ class TextTower:
         dxb = torch.zeros((C * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L)
+        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer)

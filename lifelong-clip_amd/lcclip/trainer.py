@@ -1,9 +1,10 @@
 """The online-CL optimizer step of methods/adapter_clip.py:49-107 (online_train) on the fused
 engines, plus data-parallel replication over RCCL.
 
-One step = image tower fwd -> text tower fwd -> normalise + logits + softmax + CE-on-probs
-(fwd and bwd fused in one head kernel) -> text/image tower bwd (PEFT grads only) ->
-[RCCL all-reduce of the flat PEFT-gradient buffer] -> non-finite check -> fused AdamW.
+One step = image tower fwd -> text tower fwd (this rank's prompt slice under DP) -> normalise
++ logits + softmax + CE-on-probs (fwd and bwd fused in one head kernel) -> image tower bwd
+(PEFT grads only; per-layer-group RCCL buckets launched as layers finish) -> text tower bwd ->
+non-finite check -> fused AdamW. The DP exchange is described in dp.py.
 
 All trainable tensors live in ONE flat fp32 buffer (parameters are views into it), and so do
 their gradients and the AdamW moments, so the optimizer is a single launch and the DP exchange
@@ -12,9 +13,9 @@ is a single all-reduce (1.47 MB LoRA / 7.93 MB adapter for ViT-B/16 both towers)
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from . import ops
+from .dp import DataParallel, layer_ranges
 from .adapter_clip import freeze_backbone
 from .ops import F32
 
@@ -33,16 +34,22 @@ def remap_labels(labels, class_list=None):
 
 class OnlineTrainer:
     def __init__(self, adapter_clip, lr=5e-4, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8,
-                 process_group=None, distributed=None):
+                 process_group=None, distributed=None, shard_text=True, bucket_layers=4):
         self.wrapper = adapter_clip
         self.clip = adapter_clip.model
         freeze_backbone(self.wrapper)
         self.img = self.clip.visual.tower
         self.txt = self.clip.text_tower
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
-        self.group = process_group
-        self.distributed = (dist.is_available() and dist.is_initialized()) if distributed is None else distributed
-        params = self.img.stack.trainable_params() + self.txt.stack.trainable_params()
+        self.dp = DataParallel(process_group, distributed)
+        self.distributed = self.dp.world > 1
+        self.shard_text = shard_text and self.distributed
+        self.bucket_layers = max(1, int(bucket_layers))
+        img_params = self.img.stack.trainable_params()
+        params = img_params + self.txt.stack.trainable_params()
+        n_img = sum(p.numel() for p in img_params)
+        self.img_ranges = layer_ranges(self.img.stack) if img_params else []
+        self.txt_range = (n_img, sum(p.numel() for p in params))
         dev = self.clip.logit_scale.device
         n = sum(p.numel() for p in params)
         self.numel = n
@@ -74,10 +81,15 @@ class OnlineTrainer:
         """Everything but the optimizer update. Returns (loss[1], probs[B,C])."""
         dev = self.flat_g.device
         self.flat_g.zero_()
+        dp = self.dp
+        C = tokens.shape[0]
         f_i, ci = self.img.forward(images, save=True, training=True)
-        f_t, ct = self.txt.forward(tokens, save=True, training=True)
+        if self.shard_text:
+            f_ts, ct = self.txt.forward(dp.shard_tokens(tokens), save=True, training=True)
+            f_t = dp.gather_rows(f_ts, C).contiguous()
+        else:
+            f_t, ct = self.txt.forward(tokens, save=True, training=True)
         B, E = f_i.shape
-        C = f_t.shape[0]
         img_n = torch.empty_like(f_i)
         txt_n = torch.empty_like(f_t)
         ni = torch.empty(B, dtype=F32, device=dev)
@@ -90,18 +102,38 @@ class OnlineTrainer:
         labels = labels.to(dev, torch.int64).contiguous()
         ops.clip_head(img_n, txt_n, self.logit_scale, labels, probs, dlog, loss)
         d_i = torch.empty_like(f_i)
-        d_t = torch.empty_like(f_t)
+        lo, hi, per = dp.prompt_slice(C) if self.shard_text else (0, C, C)
+        d_tp = torch.zeros(per * dp.world if self.shard_text else C, E, dtype=F32, device=dev)
         ops.head_feat_grad(dlog, C, 1, txt_n, img_n, ni, self.logit_scale, d_i)
-        ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_t)
-        if ct is not None and self.txt.stack.trainable_params():
-            self.txt.backward(ct, d_t, self.grads)
+        ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
+        train_txt = ct is not None and bool(self.txt.stack.trainable_params())
+        w_dt = dp.sum_async(d_tp) if (self.shard_text and train_txt) else None
         if self.img.stack.trainable_params():
-            self.img.backward(ci, d_i, self.grads)
+            self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook())
+        if train_txt:
+            if w_dt is not None:
+                w_dt.wait()
+            self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
+        dp.launch_bucket(self.flat_g, *self.txt_range)
         return loss, probs
 
+    def _img_bucket_hook(self):
+        """Launch the all-reduce of image layers [li, prev) every bucket_layers layers."""
+        if not self.distributed:
+            return None
+        state = {"hi": len(self.img_ranges)}
+
+        def hook(li):
+            if li % self.bucket_layers == 0:
+                lo_r = self.img_ranges[li][0]
+                hi_r = self.img_ranges[state["hi"] - 1][1]
+                self.dp.launch_bucket(self.flat_g, lo_r, hi_r)
+                state["hi"] = li
+        return hook
+
     def all_reduce_grads(self):
-        if self.distributed:
-            dist.all_reduce(self.flat_g, op=dist.ReduceOp.AVG, group=self.group)
+        """Wait for the bucketed exchange launched during backward; grads become rank means."""
+        self.dp.finish_buckets(self.flat_g)
 
     def optimizer_step(self):
         self.step_count += 1
