@@ -54,9 +54,17 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
     return x, tok.to(dev), y.to(dev)
 
 
+def routes_to_pp(M, N, K):
+    """The lc_gemm_nt tile selector's rule for the 256x256 ping-pong kernel (gemm.hip,
+    lc_gemm_nt_ex): the dominant kernel of the step."""
+    return N % 128 == 0 and M >= 4096 and N % 256 == 0 and (N >= 2048 or K >= 2048)
+
+
 class GemmTimer:
-    """Times every lc_gemm_nt launch of one step with HIP events on the launch stream and sums
-    the algorithmic FLOPs (2*M*N*K) — the dominant kernel's achieved rate."""
+    """Times every lc_gemm_nt launch of one step with HIP events on the launch stream (torch's
+    current stream, which ops.gemm_nt launches on) and sums the algorithmic FLOPs (2*M*N*K) and
+    algorithmic HBM bytes (A, B, outputs and side inputs once each) of the launches that route
+    to the ping-pong kernel."""
 
     def __init__(self, ops_mod):
         self.ops = ops_mod
@@ -71,7 +79,14 @@ class GemmTimer:
             e0.record(st)
             r = self.orig(A, B, epi, out0, **kw)
             e1.record(st)
-            self.records.append((e0, e1, 2.0 * A.shape[0] * B.shape[0] * A.shape[1]))
+            M, K = A.shape
+            N = B.shape[0]
+            nbytes = (M * K + N * K) * 2 + out0.numel() * out0.element_size()
+            for extra in ("out1", "aux"):
+                t = kw.get(extra)
+                if t is not None:
+                    nbytes += t.numel() * t.element_size()
+            self.records.append((e0, e1, 2.0 * M * N * K, nbytes, routes_to_pp(M, N, K)))
             return r
         self.ops.gemm_nt = timed
         import lcclip.engine as eng
@@ -83,11 +98,24 @@ class GemmTimer:
 
     def summary(self):
         torch.cuda.synchronize()
-        ms = sum(e0.elapsed_time(e1) for e0, e1, _ in self.records)
-        flops = sum(f for _, _, f in self.records)
-        big = [(e0.elapsed_time(e1), f) for e0, e1, f in self.records if f > 1e11]
-        return dict(n=len(self.records), ms=ms, flops=flops,
-                    big_ms=sum(t for t, _ in big), big_flops=sum(f for _, f in big), big_n=len(big))
+        ms = sum(r[0].elapsed_time(r[1]) for r in self.records)
+        pp = [(r[0].elapsed_time(r[1]), r[2], r[3]) for r in self.records if r[4]]
+        return dict(n=len(self.records), ms=ms, pp_n=len(pp), pp_ms=sum(t for t, _, _ in pp),
+                    pp_flops=sum(f for _, f, _ in pp), pp_bytes=sum(b for _, _, b in pp))
+
+
+def pmc_traffic():
+    """HBM bytes per ping-pong launch from the latest committed PMC summary
+    (tools/profile_round.sh + tools/pmc_traffic.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "gemm_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    fam = d.get("families", {}).get("gemm_pp_kernel")
+    if not fam:
+        return None, None
+    return fam["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(seconds_cap=30.0):
@@ -180,7 +208,9 @@ def main():
     if rank == 0:
         f_img = F_IMG[args.method]
         f_step = B * f_img + C * F_TXT[args.method] + 6 * B * C * 512
-        achieved = gs["big_flops"] / (gs["big_ms"] * 1e-3)
+        achieved = gs["pp_flops"] / (gs["pp_ms"] * 1e-3)
+        traffic, traffic_src = pmc_traffic()
+        n_pp = max(gs["pp_n"], 1)
         out = {
             "metric": "images/sec/GPU (ViT-B/16 fwd+bwd, bs=256) + online A_AUC on CIFAR-100",
             "value": round(total_ips, 2),
@@ -201,14 +231,19 @@ def main():
                        "text_prompts": C, "parallelism": f"dp{world}"},
             "images_per_s_per_gpu": round(total_ips / world, 2),
             "mfma_frac_step": round(f_step / (ms * 1e-3) / PEAK_BF16, 4),
-            "roofline": {"bound": "mfma", "kernel": "lc_gemm_nt (bf16 MFMA GEMM, all shapes of "
-                                                    "the step with >= 0.1 TFLOP per launch)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "gemm_pp_kernel<EPI 0|3|4> (256x256 ping-pong bf16 MFMA GEMM: "
+                                   "QKV, c_fc+QuickGELU, c_proj fwd and their dX backward)",
                          "achieved": round(achieved / 1e12, 2), "peak": PEAK_BF16 / 1e12,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4),
-                         "traffic": None,
-                         "launches_per_step": gs["big_n"],
-                         "avg_launch_ms": round(gs["big_ms"] / max(gs["big_n"], 1), 4),
-                         "gemm_share_of_step": round(gs["ms"] / ms, 3)},
+                         "traffic": None if traffic is None else round(traffic),
+                         "traffic_unit": "bytes per launch (PMC FETCH_SIZE*2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": round(gs["pp_bytes"] / n_pp),
+                         "flops_per_launch": round(gs["pp_flops"] / n_pp),
+                         "launches_per_step": gs["pp_n"],
+                         "avg_launch_ms": round(gs["pp_ms"] / n_pp, 4),
+                         "all_gemm_share_of_step": round(gs["ms"] / ms, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()

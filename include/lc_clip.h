@@ -94,7 +94,7 @@ int lc_text_embed(hipStream_t stream, int C, int L, int D, const int64_t* tokens
 /* row_idx[c] = c*L + argmax_t tokens[c][t]   (EOT pooling, model.py:953-954). */
 int lc_eot_rows(hipStream_t stream, int C, int L, const int64_t* tokens, int* row_idx);
 
-/* Multi-head attention core, d_head = 64, L <= 256 (bwd: L <= 224). qkv [n_seq*L, ldq] holds
+/* Multi-head attention core, d_head = 64, L <= 256. qkv [n_seq*L, ldq] holds
  * q|k|v at columns 0, H*64, 2*H*64; O [n_seq*L, ldo]; lse f32 [n_seq*H, L] (log2 domain).
  * causal = 1 applies the text tower's upper-triangular -inf mask.
  * Replaces: lora.py:950-1071 (q scaling, bmm, mask, softmax, dropout p=0, bmm) and the SDPA
