@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--classes", type=int, default=10)
     ap.add_argument("--method", default="adapter", choices=["adapter", "lora", "vanilla"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a HIP graph (1 GPU; measured equal to eager at B=256)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -177,6 +179,7 @@ def main():
     trainer = OnlineTrainer(model, distributed=world > 1)
     B, C = args.batch, args.classes
     x, tok, y = synthetic_batch(B, C, dev, seed=100 + rank)
+    graph = trainer.enable_graph(x, y, tok) if args.graph else False
 
     for _ in range(args.warmup):
         trainer.step(x, y, tok)
@@ -202,7 +205,7 @@ def main():
     # dominant kernel (lc_gemm_nt family) timed live with HIP events on its launch stream,
     # over one extra, untimed step
     with GemmTimer(ops) as gt:
-        trainer.step(x, y, tok)
+        trainer.eager_step(x, y, tok)
     gs = gt.summary()
 
     if rank == 0:
@@ -228,7 +231,8 @@ def main():
             "config": {"workload": f"{args.method}_clip ViT-B/16 both towers, online_train step "
                                    f"(fwd + CE-on-probs + bwd + AdamW)",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": 197,
-                       "text_prompts": C, "parallelism": f"dp{world}"},
+                       "text_prompts": C, "parallelism": f"dp{world}",
+                       "launch": "hip_graph" if graph else "eager"},
             "images_per_s_per_gpu": round(total_ips / world, 2),
             "mfma_frac_step": round(f_step / (ms * 1e-3) / PEAK_BF16, 4),
             "roofline": {"bound": "mfma",

@@ -121,11 +121,14 @@ int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY,
                  float* dA, float* dB);
 
 /* xout = resid + z + scale*(drop(relu(z Wd^T + bd)) Wu^T + bu); h (bf16 [M,64]) is saved.
- * keep = 1 - dropout p; seed selects the counter-based dropout mask.
+ * keep = 1 - dropout p; the counter-based dropout mask is selected by
+ * seed + (*seed_dev) * const when seed_dev != NULL (a device-side RNG epoch, so a captured HIP
+ * graph draws fresh masks on every replay), else by seed alone.
  * Replaces: Adapter.forward (adapter.py:53-72) + the block residual (model.py:440-441). */
 int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
                    const float* bd, const void* Wu, const float* bu, float scale, float keep,
-                   unsigned long long seed, const float* resid, float* xout, long ldx, void* h);
+                   unsigned long long seed, const unsigned long long* seed_dev,
+                   const float* resid, float* xout, long ldx, void* h);
 
 /* Row-local adapter backward: dpre (bf16 [M,64]) and dz = gout + dpre Wd (bf16).
  * WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16). Weight/bias gradients: lc_gemm_tn.
@@ -137,10 +140,16 @@ int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg,
 /* *flag |= any(!isfinite(g))  (GradScaler's inf check, _trainer.py:163, adapter_clip.py:94). */
 int lc_check_finite(hipStream_t stream, long n, const float* g, int* flag);
 
-/* torch.optim.AdamW step over a flat fp32 buffer; skipped when *skip != 0.
+/* torch.optim.AdamW step over a flat fp32 buffer; skipped when *skip != 0. The bias-correction
+ * step is `step`, or *step_dev when step_dev != NULL (device-side counter, graph replay).
  * Replaces: optimizer.step() (utils/train_utils.py:27-28, methods/adapter_clip.py:94). */
 int lc_adamw(hipStream_t stream, long n, float* p, const float* g, float* m, float* v, float lr,
-             float b1, float b2, float eps, float wd, int step, const int* skip);
+             float b1, float b2, float eps, float wd, int step, const int* skip,
+             const long long* step_dev);
+
+/* ctr[i] += delta for i < n (n <= 64): the per-step device counters (RNG epoch, AdamW step) a
+ * captured step graph advances on every replay. */
+int lc_counter_add(hipStream_t stream, int n, long long* ctr, long long delta);
 
 /* out[r] = f[r] / ||f[r]||, norms[r] = ||f[r]||   (model.py:966-969, adapter_clip.py:78). */
 int lc_l2norm_rows(hipStream_t stream, int R, int E, const float* f, long ldf, float* out,

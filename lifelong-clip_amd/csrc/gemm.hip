@@ -117,6 +117,9 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
     }
   };
   if constexpr (AUXF || AUXB) prefetch(0, 0);
+  uint64_t seed = ep.seed;
+  if constexpr (EPI == EPI_AD_DOWN)
+    if (ep.seed_dev) seed += *ep.seed_dev * 0xD1B54A32D192ED03ull;
 #pragma unroll
   for (int pass = 0; pass < WT_M / PASS; ++pass) {
 #pragma unroll
@@ -161,7 +164,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
             uint2{pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
       } else if constexpr (EPI == EPI_AD_DOWN) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f) * drop_mul(ep.seed, m, n + r, ep.keep);
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f) * drop_mul(seed, m, n + r, ep.keep);
         *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
             uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
       } else if constexpr (EPI == EPI_AD_UP) {

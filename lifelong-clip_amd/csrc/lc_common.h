@@ -46,10 +46,19 @@ LC_DEV float wave_max(float v) {
   return v;
 }
 
-LC_DEV float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+// QuickGELU (model.py:203-206): x * sigmoid(1.702 x), with the sigmoid as one v_exp_f32 and one
+// v_rcp_f32 (1 ulp) — the IEEE division would cost ~10 VALU per element in the GEMM epilogues.
+// exp2(-1.702*log2(e)*x) overflows to +inf for very negative x: rcp(inf) = 0, the right limit.
+constexpr float LC_GELU_K2 = -1.702f * 1.4426950408889634f;
+LC_DEV float lc_sigmoid1702(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(LC_GELU_K2 * x));
+}
+LC_DEV float quick_gelu(float x) { return x * lc_sigmoid1702(x); }
+// d/dx [x s(x)] = s + 1.702 x s (1 - s) = s * (1 + t (1 - s)),  t = 1.702 x
 LC_DEV float quick_gelu_grad(float x) {
-  float s = 1.0f / (1.0f + __expf(-1.702f * x));
-  return s + 1.702f * x * s * (1.0f - s);
+  const float s = lc_sigmoid1702(x);
+  const float t = 1.702f * x;
+  return s * __builtin_fmaf(t, 1.0f - s, 1.0f);
 }
 
 // Counter-based hash RNG (splitmix-style) for adapter dropout masks: mask(seed, index) is a
@@ -78,6 +87,7 @@ struct EpiParams {
   float keep;        // 1 - dropout p
   uint64_t seed;     // dropout mask seed
   unsigned long long* dbg;  // diagnostic timestamps (nullptr in production)
+  const unsigned long long* seed_dev;  // optional device-side RNG epoch added to seed (graphs)
 };
 
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).

@@ -197,8 +197,13 @@ __global__ void finite_kernel(long n, const float* __restrict__ g, int* __restri
 __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, float lr, float b1,
                              float b2, float eps, float wd, float bc1, float bc2,
-                             const int* __restrict__ skip) {
+                             const int* __restrict__ skip, const long long* __restrict__ step_dev) {
   if (skip && *skip) return;
+  if (step_dev) {  // bias corrections from the device-side step counter (graph replay)
+    const float st = (float)*step_dev;
+    bc1 = 1.0f - powf(b1, st);
+    bc2 = 1.0f - powf(b2, st);
+  }
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i];
     float pi = p[i] * (1.0f - lr * wd);
@@ -209,6 +214,10 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
     const float denom = sqrtf(vi / bc2) + eps;
     p[i] = pi - (lr / bc1) * mi / denom;
   }
+}
+
+__global__ void counter_add_kernel(int n, long long* ctr, long long delta) {
+  if ((int)threadIdx.x < n) ctr[threadIdx.x] += delta;
 }
 
 int grid_for(long work, int block) {
@@ -259,10 +268,11 @@ int lc_lora_grad(hipStream_t st, int M, int N, int K, int r, const void* dY, lon
 //   xout = resid + z + scale * (h Wu^T + bu)       [M,D]   N = D,   K = 64
 int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
                    const float* bd, const void* Wu, const float* bu, float scale, float keep,
-                   unsigned long long seed, const float* resid, float* xout, long ldx, void* hout) {
+                   unsigned long long seed, const unsigned long long* seed_dev,
+                   const float* resid, float* xout, long ldx, void* hout) {
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldz % 8 == 0 && ldx % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  EpiParams ep{z, ldz, scale, keep, (uint64_t)seed, nullptr};
+  EpiParams ep{z, ldz, scale, keep, (uint64_t)seed, nullptr, seed_dev};
   int rc = lc_gemm_nt_ex(st, 6 /*EPI_AD_DOWN*/, M, AD_H, D, z, ldz, Wd, D, bd, 1.0f, hout, AD_H,
                          nullptr, 0, nullptr, 0, ep);
   if (rc) return rc;
@@ -293,12 +303,20 @@ int lc_check_finite(hipStream_t st, long n, const float* g, int* flag) {
 }
 
 int lc_adamw(hipStream_t st, long n, float* p, const float* g, float* m, float* v, float lr,
-             float b1, float b2, float eps, float wd, int step, const int* skip) {
-  LC_CHECK_ARG(n >= 0 && step >= 1);
+             float b1, float b2, float eps, float wd, int step, const int* skip,
+             const long long* step_dev) {
+  LC_CHECK_ARG(n >= 0 && (step >= 1 || step_dev != nullptr));
   if (n == 0) return LC_OK;
-  const float bc1 = 1.0f - powf(b1, (float)step), bc2 = 1.0f - powf(b2, (float)step);
+  const float fs = (float)(step >= 1 ? step : 1);
+  const float bc1 = 1.0f - powf(b1, fs), bc2 = 1.0f - powf(b2, fs);
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, n, p, g, m, v, lr, b1,
-                     b2, eps, wd, bc1, bc2, skip);
+                     b2, eps, wd, bc1, bc2, skip, step_dev);
+  LC_LAUNCH_RET();
+}
+
+int lc_counter_add(hipStream_t st, int n, long long* ctr, long long delta) {
+  LC_CHECK_ARG(n > 0 && n <= 64 && ctr != nullptr);
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, st, n, ctr, delta);
   LC_LAUNCH_RET();
 }
 

@@ -35,10 +35,11 @@ SIGNATURES = {
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
     "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
-                       c_long, P],
+                       P, c_long, P],
     "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long],
     "lc_check_finite": [P, c_long, P, P],
-    "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P],
+    "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P, P],
+    "lc_counter_add": [P, c_int, P, c_long],
     "lc_l2norm_rows": [P, c_int, c_int, P, c_long, P, P],
     "lc_clip_head": [P, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "lc_head_logits": [P, c_int, c_int, c_int, P, P, P, P, P],

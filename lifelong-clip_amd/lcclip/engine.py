@@ -58,6 +58,8 @@ class BlockStack:
         self.causal = bool(causal)
         self.variant = variant  # 'vanilla' | 'lora' | 'adapter'
         self.staged = [StagedBlock() for _ in self.blocks]
+        # optional int64 device tensor: RNG epoch added to every dropout seed (graph replay)
+        self.seed_dev = None
 
     # ------------------------------------------------------------------ weight staging
     def trainable_params(self):
@@ -71,6 +73,13 @@ class BlockStack:
         for b in self.blocks:
             out.extend(b.backbone_parameters())
         return out
+
+    def invalidate_peft(self):
+        """Forget the staged PEFT-derived weights (LoRA merges, adapter bf16 copies). Needed after
+        any update that bypasses torch's version counters (the fused AdamW writes the flat
+        parameter buffer through the C ABI)."""
+        for st in self.staged:
+            st.peft_key = None
 
     def stage(self):
         for blk, st in zip(self.blocks, self.staged):
@@ -150,7 +159,7 @@ class BlockStack:
                 ops.gemm_nt(O, st.wo, EPI_BF16, z1, bias=blk.attn.out_proj.bias)
                 hd1 = _empty((M, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale, keep,
-                                seed1, x, x_mid, hd1)
+                                seed1, x, x_mid, hd1, seed_dev=self.seed_dev)
                 s.update(z1=z1, hd1=hd1, keep=keep)
             else:
                 ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
@@ -167,7 +176,7 @@ class BlockStack:
                 ops.gemm_nt(tmp_g, st.wpr, EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
                 hd2 = _empty((M, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
-                                s["keep"], seed2, x_mid, x_out, hd2)
+                                s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
                 ops.gemm_nt(tmp_g, st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)

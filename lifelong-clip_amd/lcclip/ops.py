@@ -138,11 +138,11 @@ def lora_grad(dY, X, A, B, scaling, dA, dB):
          X.stride(0), ptr(A), ptr(B), float(scaling), ptr(dA), ptr(dB))
 
 
-def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h):
+def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=None):
     M, D = z.shape
     call("lc_adapter_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
-         ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(resid), ptr(xout),
-         xout.stride(0), ptr(h))
+         ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
+         ptr(resid), ptr(xout), xout.stride(0), ptr(h))
 
 
 def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
@@ -155,9 +155,16 @@ def check_finite(g, flag):
     call("lc_check_finite", stream_of(g), g.numel(), ptr(g), ptr(flag))
 
 
-def adamw(p, g, m, v, lr, b1, b2, eps, wd, step, skip=None):
+def adamw(p, g, m, v, lr, b1, b2, eps, wd, step, skip=None, step_dev=None):
     call("lc_adamw", stream_of(p), p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), float(lr), float(b1),
-         float(b2), float(eps), float(wd), int(step), ptr(skip))
+         float(b2), float(eps), float(wd), int(step), ptr(skip), ptr(step_dev))
+
+
+def counter_add(ctr, delta=1):
+    """ctr (int64 device tensor, <= 64 entries) += delta, on the current stream."""
+    if ctr.dtype != torch.int64 or not ctr.is_contiguous():
+        raise ValueError("counters must be a contiguous int64 tensor")
+    call("lc_counter_add", stream_of(ctr), ctr.numel(), ptr(ctr), int(delta))
 
 
 def l2norm_rows(f, out, norms):

@@ -69,6 +69,7 @@ class OnlineTrainer:
         self.params = params
         self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_count = 0
+        self.graph = None
         self.logit_scale = self.clip.logit_scale.detach().reshape(1)
 
     def reset_optimizer(self):
@@ -76,6 +77,8 @@ class OnlineTrainer:
         self.m.zero_()
         self.v.zero_()
         self.step_count = 0
+        if self.graph is not None:
+            self.ctr[1].zero_()
 
     def forward_backward(self, images, labels, tokens):
         """Everything but the optimizer update. Returns (loss[1], probs[B,C])."""
@@ -142,9 +145,81 @@ class OnlineTrainer:
         b1, b2 = self.betas
         ops.adamw(self.flat_p, self.flat_g, self.m, self.v, self.lr, b1, b2, self.eps, self.wd,
                   self.step_count, self.skip)
+        # the update bypassed torch's version counters: re-stage the PEFT-derived weights
+        self.img.stack.invalidate_peft()
+        self.txt.stack.invalidate_peft()
 
     def step(self, images, labels, tokens):
+        if self.graph is not None:
+            return self._replay(images, labels, tokens)
+        return self.eager_step(images, labels, tokens)
+
+    def eager_step(self, images, labels, tokens):
+        """One step launched op by op (also available when a graph is active, e.g. to time the
+        individual kernels)."""
         loss, probs = self.forward_backward(images, labels, tokens)
         self.all_reduce_grads()
         self.optimizer_step()
         return loss, probs
+
+    # ------------------------------------------------------------------ HIP graph replay
+    def enable_graph(self, images, labels, tokens, warmup=2):
+        """Capture one whole step (fwd, head, bwd, non-finite check, AdamW) as a HIP graph and
+        replay it from then on: the ~650 launches of a step leave the host once, with no
+        inter-kernel gaps. Shapes are fixed at capture; `images` / `labels` / `tokens` become the
+        graph's input buffers (a later step() with other tensors copies into them). The dropout
+        masks and AdamW's bias correction read device-side counters that the graph advances on
+        every replay. Single process only: under torch.distributed the step stays eager.
+        Returns True when the graph is active."""
+        if self.distributed:
+            return False
+        dev = self.flat_p.device
+        self._gx = images
+        self._gy = labels.to(dev, torch.int64).contiguous()
+        self._gt = tokens.contiguous()
+        self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)  # [rng epoch, adam step]
+        self.ctr[1] = self.step_count
+        for st in (self.img.stack, self.txt.stack):
+            st.seed_dev = self.ctr[0:1]
+        # warm-up steps (allocator, lazy staging) must not change the model: snapshot + restore
+        snap = [t.clone() for t in (self.flat_p, self.m, self.v, self.ctr)]
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._graph_body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        for t, c in zip((self.flat_p, self.m, self.v, self.ctr), snap):
+            t.copy_(c)
+        self.img.stack.invalidate_peft()
+        self.txt.stack.invalidate_peft()
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._g_out = self._graph_body()
+        self.graph = g
+        return True
+
+    def _graph_body(self):
+        ops.counter_add(self.ctr, 1)
+        loss, probs = self.forward_backward(self._gx, self._gy, self._gt)
+        self.skip.zero_()
+        ops.check_finite(self.flat_g, self.skip)
+        b1, b2 = self.betas
+        ops.adamw(self.flat_p, self.flat_g, self.m, self.v, self.lr, b1, b2, self.eps, self.wd, 1,
+                  self.skip, step_dev=self.ctr[1:2])
+        # captured merges must re-run on every replay: stage again inside the next capture/run
+        self.img.stack.invalidate_peft()
+        self.txt.stack.invalidate_peft()
+        return loss, probs
+
+    def _replay(self, images, labels, tokens):
+        if images.data_ptr() != self._gx.data_ptr():
+            self._gx.copy_(images)
+        if labels.data_ptr() != self._gy.data_ptr():
+            self._gy.copy_(labels.to(self._gy.device, torch.int64))
+        if tokens.data_ptr() != self._gt.data_ptr():
+            self._gt.copy_(tokens)
+        self.graph.replay()
+        self.step_count += 1
+        return self._g_out

@@ -200,3 +200,55 @@ def test_vit_b16_batch256_properties(dev):
         f1, _ = tr.img.forward(img[:8], save=False)
         f2, _ = tr.img.forward(img[:8], save=False)
     assert torch.equal(f1, f2)
+
+
+@pytest.mark.parametrize("method", ["lora", "adapter"])
+def test_multi_step_staging_tracks_updates(golden, dev, method):
+    """After several fused optimizer steps (large lr so the PEFT weights move a lot), the next
+    forward must use the CURRENT parameters: compare with the oracle evaluated on the trainer's
+    parameters as they are now (catches stale LoRA merges / adapter bf16 copies)."""
+    from lcclip import OnlineTrainer
+    from oracle import clip_oracle as o
+    d, sd = golden
+    w = make_wrapper(sd, method, "both", dev)
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    tr = OnlineTrainer(w, lr=5e-2)
+    for _ in range(3):
+        tr.step(img, y, tok)
+    _, probs = tr.forward_backward(img, y, tok)
+    now = {n: p.detach().cpu().float() for n, p in w.model.state_dict().items()}
+    moved = max((now[n] - sd[n]).abs().max().item() for n in now if o.is_trainable(n))
+    assert moved > 1e-2  # the PEFT weights did move
+    ref, _, _ = o.adapter_clip_forward(img.cpu(), tok.cpu(), now, o.TINY, method, "both",
+                                       rt=o.round_bf16)
+    err = (probs.cpu() - ref).abs().max().item()
+    record(test="multi_step_staging", method=method, probs_abs_vs_bf16_oracle=err, moved=moved)
+    assert err < 4e-3
+
+
+@pytest.mark.parametrize("method", ["lora", "adapter"])
+def test_graph_replay_matches_eager(golden, dev, method):
+    """The captured step (HIP graph) computes what the op-by-op step computes, replay after
+    replay; its warm-up leaves the model untouched and its device counters advance per replay."""
+    from lcclip import OnlineTrainer
+    d, sd = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    te = OnlineTrainer(make_wrapper(sd, method, "both", dev), lr=5e-3)
+    tg = OnlineTrainer(make_wrapper(sd, method, "both", dev), lr=5e-3)
+    p0 = tg.flat_p.clone()
+    assert tg.enable_graph(img, y, tok)
+    assert torch.equal(tg.flat_p, p0)  # warm-up restored
+    for _ in range(3):
+        le, pe = te.step(img, y, tok)
+        lg, pg = tg.step(img, y, tok)
+        torch.cuda.synchronize()
+        assert abs(le.item() - lg.item()) < 1e-5
+        assert (pe - pg).abs().max().item() < 1e-5
+    r = ((tg.flat_p - te.flat_p).norm() / (te.flat_p - p0).norm()).item()
+    record(test="graph_vs_eager", method=method, param_delta_rel=r)
+    assert r < 1e-3
+    assert tg.ctr.tolist() == [3, 3]
