@@ -36,6 +36,9 @@ extern "C" {
 #define LC_EPI_GELU 3     /* out0 bf16 = acc + bias; out1 bf16 = QuickGELU(acc + bias)        */
 #define LC_EPI_GELU_BWD 4 /* out0 bf16 = alpha*acc * QuickGELU'(aux_bf16)                    */
 #define LC_EPI_BF16_F32 5 /* out0 bf16 and out1 f32 of alpha*acc + bias                     */
+#define LC_EPI_GELU_D 6   /* out0 bf16 = QuickGELU'(pre); out1 bf16 = QuickGELU(pre), pre =    */
+                          /* acc + bias: saves the derivative for the backward, not pre        */
+#define LC_EPI_MUL 7      /* out0 bf16 = alpha*acc * aux_bf16   (dX of c_fc with saved GELU')  */
 
 /* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0.
  * Replaces: F.linear for QKV / out-proj (models/clip/lora.py:837, 1072; torch MHA for

@@ -28,11 +28,13 @@ enum {
   EPI_GELU = 3,        // out0 bf16 = pre = acc+bias ; out1 bf16 = quick_gelu(pre)
   EPI_GELU_BWD = 4,    // out0 bf16 = (acc*alpha) * quick_gelu'(aux_bf16)
   EPI_BF16_F32 = 5,    // out0 bf16 and out1 f32 of acc*alpha + bias
+  EPI_GELU_D = 6,      // out0 bf16 = quick_gelu'(pre) ; out1 bf16 = quick_gelu(pre), pre = acc+bias
+  EPI_MUL = 7,         // out0 bf16 = (acc*alpha) * aux_bf16
   // fused adapter epilogues (internal; adapter.py:59-72 as two skinny GEMMs)
-  EPI_AD_DOWN = 6,     // out0 bf16 = relu(acc + bias) * dropmask(seed, m, n) / keep
-  EPI_AD_UP = 7,       // out0 f32 = aux_f32 + aux2_bf16 + scale * (acc + bias)
-  EPI_AD_MASK = 8,     // out0 bf16 = aux_bf16 > 0 ? alpha * acc / keep : 0
-  EPI_AD_ADD = 9,      // out0 bf16 = aux_bf16 + acc
+  EPI_AD_DOWN = 8,     // out0 bf16 = relu(acc + bias) * dropmask(seed, m, n) / keep
+  EPI_AD_UP = 9,       // out0 f32 = aux_f32 + aux2_bf16 + scale * (acc + bias)
+  EPI_AD_MASK = 10,    // out0 bf16 = aux_bf16 > 0 ? alpha * acc / keep : 0
+  EPI_AD_ADD = 11,     // out0 bf16 = aux_bf16 + acc
 };
 
 namespace {
@@ -95,13 +97,15 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   const int lc = (lane % LPR) * 4;
   const int n = n0 + wn * WT_N + lc;
   float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (EPI != EPI_GELU_BWD && EPI != EPI_AD_MASK && EPI != EPI_AD_ADD && bias != nullptr)
+  if (EPI != EPI_GELU_BWD && EPI != EPI_MUL && EPI != EPI_AD_MASK && EPI != EPI_AD_ADD &&
+      bias != nullptr)
     bb = *reinterpret_cast<const float4*>(bias + n);
   // side inputs (residual / pre-activation / adapter z / h) of a pass are fetched one pass
   // ahead, before the stores of the current pass: CDNA's vmcnt also counts stores, so a load
   // issued after them would wait for their acknowledgement.
   constexpr bool AUXF = (EPI == EPI_RESID || EPI == EPI_AD_UP);
-  constexpr bool AUXB = (EPI == EPI_GELU_BWD || EPI == EPI_AD_MASK || EPI == EPI_AD_ADD);
+  constexpr bool AUXB = (EPI == EPI_GELU_BWD || EPI == EPI_MUL || EPI == EPI_AD_MASK ||
+                         EPI == EPI_AD_ADD);
   constexpr bool AUX2 = (EPI == EPI_AD_UP);
   constexpr int NIT = PASS / RPI;
   float4 pf_f[2][NIT];
@@ -162,6 +166,23 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
         const float g2 = quick_gelu_grad(bf2f(a.y & 0xffff)), g3 = quick_gelu_grad(bf2f(a.y >> 16));
         *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
             uint2{pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
+      } else if constexpr (EPI == EPI_GELU_D) {
+        float gg[4], dd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float sg = lc_sigmoid1702(v[r]);
+          gg[r] = v[r] * sg;
+          dd[r] = sg * __builtin_fmaf(1.702f * v[r], 1.0f - sg, 1.0f);
+        }
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(dd[0], dd[1]), pack2bf(dd[2], dd[3])};
+        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) =
+            uint2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])};
+      } else if constexpr (EPI == EPI_MUL) {
+        const uint2 a = xb;
+        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
+            uint2{pack2bf(v[0] * bf2f(a.x & 0xffff), v[1] * bf2f(a.x >> 16)),
+                  pack2bf(v[2] * bf2f(a.y & 0xffff), v[3] * bf2f(a.y >> 16))};
       } else if constexpr (EPI == EPI_AD_DOWN) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f) * drop_mul(seed, m, n + r, ep.keep);
@@ -553,6 +574,8 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
     LC_NT_CASE(EPI_GELU)
     LC_NT_CASE(EPI_GELU_BWD)
     LC_NT_CASE(EPI_BF16_F32)
+    LC_NT_CASE(EPI_GELU_D)
+    LC_NT_CASE(EPI_MUL)
     LC_NT_CASE(EPI_AD_DOWN)
     LC_NT_CASE(EPI_AD_UP)
     LC_NT_CASE(EPI_AD_MASK)
@@ -581,6 +604,8 @@ int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
     LC_PP_CASE(EPI_GELU)
     LC_PP_CASE(EPI_GELU_BWD)
     LC_PP_CASE(EPI_BF16_F32)
+    LC_PP_CASE(EPI_GELU_D)
+    LC_PP_CASE(EPI_MUL)
     LC_PP_CASE(EPI_AD_DOWN)
     LC_PP_CASE(EPI_AD_UP)
     LC_PP_CASE(EPI_AD_MASK)
@@ -609,9 +634,10 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
   LC_CHECK_ARG(ldo0 % 4 == 0 && ldo0 >= N);
-  LC_CHECK_ARG(epi >= 0 && epi <= 9);
-  if (epi == EPI_GELU || epi == EPI_BF16_F32) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
-  if (epi == EPI_RESID || epi == EPI_GELU_BWD || epi >= EPI_AD_UP)
+  LC_CHECK_ARG(epi >= 0 && epi <= EPI_AD_ADD);
+  if (epi == EPI_GELU || epi == EPI_BF16_F32 || epi == EPI_GELU_D)
+    LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
+  if (epi == EPI_RESID || epi == EPI_GELU_BWD || epi == EPI_MUL || epi >= EPI_AD_UP)
     LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 4 == 0);
   if (epi == EPI_AD_UP) LC_CHECK_ARG(ep.aux2 != nullptr && ep.ldaux2 >= N && ep.ldaux2 % 4 == 0);
   auto a = static_cast<const bf16_t*>(A);
@@ -656,7 +682,7 @@ extern "C" {
 int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux) {
-  LC_CHECK_ARG(epi >= 0 && epi <= 5);
+  LC_CHECK_ARG(epi >= 0 && epi <= 7);
   EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
   return lc_gemm_nt_ex(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                        aux, ldaux, ep);

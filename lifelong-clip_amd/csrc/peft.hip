@@ -273,10 +273,10 @@ int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const 
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldz % 8 == 0 && ldx % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
   EpiParams ep{z, ldz, scale, keep, (uint64_t)seed, nullptr, seed_dev};
-  int rc = lc_gemm_nt_ex(st, 6 /*EPI_AD_DOWN*/, M, AD_H, D, z, ldz, Wd, D, bd, 1.0f, hout, AD_H,
+  int rc = lc_gemm_nt_ex(st, 8 /*EPI_AD_DOWN*/, M, AD_H, D, z, ldz, Wd, D, bd, 1.0f, hout, AD_H,
                          nullptr, 0, nullptr, 0, ep);
   if (rc) return rc;
-  return lc_gemm_nt_ex(st, 7 /*EPI_AD_UP*/, M, D, AD_H, hout, AD_H, Wu, AD_H, bu, 1.0f, xout, ldx,
+  return lc_gemm_nt_ex(st, 9 /*EPI_AD_UP*/, M, D, AD_H, hout, AD_H, Wu, AD_H, bu, 1.0f, xout, ldx,
                        nullptr, 0, resid, ldx, ep);
 }
 
@@ -288,10 +288,10 @@ int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, con
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 4 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
   EpiParams ep{nullptr, 0, scale, keep, 0, nullptr};
-  int rc = lc_gemm_nt_ex(st, 8 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
+  int rc = lc_gemm_nt_ex(st, 10 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
                          AD_H, nullptr, 0, h, AD_H, ep);
   if (rc) return rc;
-  return lc_gemm_nt_ex(st, 9 /*EPI_AD_ADD*/, M, D, AD_H, dpre, AD_H, WdT, AD_H, nullptr, 1.0f, dz,
+  return lc_gemm_nt_ex(st, 11 /*EPI_AD_ADD*/, M, D, AD_H, dpre, AD_H, WdT, AD_H, nullptr, 1.0f, dz,
                        ldz, nullptr, 0, gout, ldg, ep);
 }
 

@@ -27,7 +27,7 @@ import itertools
 import torch
 
 from . import ops
-from .ops import BF16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_BWD, EPI_RESID
+from .ops import BF16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_D, EPI_MUL, EPI_RESID
 
 _seed_counter = itertools.count(1)
 
@@ -167,7 +167,9 @@ class BlockStack:
             rstd2 = _empty((M,), F32, dev)
             ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, tmp_h, mean2, rstd2)
             pre = _empty((M, 4 * D), BF16, dev) if save else tmp_pre
-            ops.gemm_nt(tmp_h, st.wfc, EPI_GELU, pre, bias=blk.mlp.c_fc.bias, out1=tmp_g)
+            # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
+            ops.gemm_nt(tmp_h, st.wfc, EPI_GELU_D if save else EPI_GELU, pre,
+                        bias=blk.mlp.c_fc.bias, out1=tmp_g)
             x_out = _empty((M, D), F32, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
@@ -182,7 +184,7 @@ class BlockStack:
                 ops.gemm_nt(tmp_g, st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
-                         mean2=mean2, rstd2=rstd2, pre=pre)
+                         mean2=mean2, rstd2=rstd2, gd=pre)
                 if self.variant == "lora":
                     s["h1"] = h1
                 saved.append(s)
@@ -213,7 +215,7 @@ class BlockStack:
                 dY = self._adapter_bwd(blk, st, dxb, s["hd2"], s["z2"], s["keep"], dz, grads)
             else:
                 dY = dxb
-            ops.gemm_nt(dY, st.wprT, EPI_GELU_BWD, da, aux=s["pre"])
+            ops.gemm_nt(dY, st.wprT, EPI_MUL, da, aux=s["gd"])
             ops.gemm_nt(da, st.wfcT, EPI_BF16, dh)
             ops.layernorm_bwd(dh, s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight, dx_mid,
                               dx_midb, dres=dx)

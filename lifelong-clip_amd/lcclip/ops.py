@@ -9,7 +9,7 @@ from ._lib import call, ptr, stream_of
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32 = range(6)
+EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32, EPI_GELU_D, EPI_MUL = range(8)
 
 
 def _rowmajor(t, dtype, name):

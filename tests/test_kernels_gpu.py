@@ -65,6 +65,15 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
     ob = torch.empty(M, N, device=dev, dtype=BF)
     ops.gemm_nt(A, B, ops.EPI_GELU_BWD, ob, alpha=0.5, aux=aux)
     assert rel(ob, 0.5 * (A.float() @ B.float().t()) * dg) < 4e-3
+    # derivative-saving forward epilogue and the multiply epilogue of its backward
+    gd = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_GELU_D, gd, bias=bias, out1=gl)
+    sr = torch.sigmoid(1.702 * ref)
+    assert rel(gl, ref * sr) < 4e-3
+    assert rel(gd, sr + 1.702 * ref * sr * (1 - sr)) < 4e-3
+    om = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_MUL, om, alpha=0.5, aux=aux)
+    assert rel(om, 0.5 * (A.float() @ B.float().t()) * a) < 4e-3
     # strided A view (row stride > K)
     Aw = torch.randn(M, K + 64, device=dev).to(BF)[:, 64:]
     ops.gemm_nt(Aw, B, ops.EPI_F32, o32)

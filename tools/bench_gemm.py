@@ -12,8 +12,8 @@ from lcclip import _lib, ops  # noqa: E402
 M = int(os.environ.get("M", 50432))
 SHAPES = [  # (name, N, K, epi)
     ("qkv_fwd", 2304, 768, ops.EPI_BF16), ("out_fwd", 768, 768, ops.EPI_BF16),
-    ("fc1_fwd", 3072, 768, ops.EPI_GELU), ("fc2_fwd", 768, 3072, ops.EPI_BF16),
-    ("fc2_dx", 3072, 768, ops.EPI_GELU_BWD), ("fc1_dx", 768, 3072, ops.EPI_BF16),
+    ("fc1_fwd", 3072, 768, ops.EPI_GELU_D), ("fc2_fwd", 768, 3072, ops.EPI_BF16),
+    ("fc2_dx", 3072, 768, ops.EPI_MUL), ("fc1_dx", 768, 3072, ops.EPI_BF16),
     ("out_dx", 768, 768, ops.EPI_BF16), ("qkv_dx", 768, 2304, ops.EPI_BF16),
 ]
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3").split(",")]
@@ -38,9 +38,9 @@ for rnd in range(3):
             a = A[:, :K]
             b = Bw[:N, :K]
             kw = {}
-            if epi == ops.EPI_GELU:
+            if epi in (ops.EPI_GELU, ops.EPI_GELU_D):
                 kw = dict(bias=bias[:N], out1=o1[:, :N])
-            elif epi == ops.EPI_GELU_BWD:
+            elif epi in (ops.EPI_GELU_BWD, ops.EPI_MUL):
                 kw = dict(aux=aux[:, :N])
             else:
                 kw = dict(bias=bias[:N])
