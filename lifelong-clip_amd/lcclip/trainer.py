@@ -20,6 +20,14 @@ from .adapter_clip import freeze_backbone
 from .ops import F32
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def remap_labels(labels, class_list=None):
     """methods/adapter_clip.py:53-61, 75-76 with visible_classes='batch': the class list is the
     distinct labels in first-seen order and y becomes an index into it. Under DP every rank
@@ -34,7 +42,8 @@ def remap_labels(labels, class_list=None):
 
 class OnlineTrainer:
     def __init__(self, adapter_clip, lr=5e-4, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8,
-                 process_group=None, distributed=None, shard_text=True, bucket_layers=4):
+                 process_group=None, distributed=None, shard_text=True, bucket_layers=4,
+                 overlap_text=True):
         self.wrapper = adapter_clip
         self.clip = adapter_clip.model
         freeze_backbone(self.wrapper)
@@ -70,6 +79,8 @@ class OnlineTrainer:
         self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
         self.step_count = 0
         self.graph = None
+        self.overlap_text = bool(overlap_text)
+        self._side = None
         self.logit_scale = self.clip.logit_scale.detach().reshape(1)
 
     def reset_optimizer(self):
@@ -81,17 +92,27 @@ class OnlineTrainer:
             self.ctr[1].zero_()
 
     def forward_backward(self, images, labels, tokens):
-        """Everything but the optimizer update. Returns (loss[1], probs[B,C])."""
+        """Everything but the optimizer update. Returns (loss[1], probs[B,C]).
+
+        The text tower (C prompts x 77 tokens: small, latency-bound launches) runs on a side HIP
+        stream concurrently with the image tower, forward and backward; the two meet at the
+        logit head and again before the gradient exchange/optimizer (`overlap_text`)."""
         dev = self.flat_g.device
         self.flat_g.zero_()
         dp = self.dp
         C = tokens.shape[0]
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev)
+        if side is not None:
+            side.wait_stream(main)
+        tok_in = dp.shard_tokens(tokens) if self.shard_text else tokens
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            f_t, ct = self.txt.forward(tok_in, save=True, training=True)
         f_i, ci = self.img.forward(images, save=True, training=True)
+        if side is not None:
+            main.wait_stream(side)
         if self.shard_text:
-            f_ts, ct = self.txt.forward(dp.shard_tokens(tokens), save=True, training=True)
-            f_t = dp.gather_rows(f_ts, C).contiguous()
-        else:
-            f_t, ct = self.txt.forward(tokens, save=True, training=True)
+            f_t = dp.gather_rows(f_t, C).contiguous()
         B, E = f_i.shape
         img_n = torch.empty_like(f_i)
         txt_n = torch.empty_like(f_t)
@@ -111,14 +132,26 @@ class OnlineTrainer:
         ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
         train_txt = ct is not None and bool(self.txt.stack.trainable_params())
         w_dt = dp.sum_async(d_tp) if (self.shard_text and train_txt) else None
+        if train_txt:
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                if w_dt is not None:
+                    w_dt.wait()  # makes the text stream wait for the dL/dT all-reduce
+                self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
         if self.img.stack.trainable_params():
             self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook())
-        if train_txt:
-            if w_dt is not None:
-                w_dt.wait()
-            self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
+        if side is not None:
+            main.wait_stream(side)
         dp.launch_bucket(self.flat_g, *self.txt_range)
         return loss, probs
+
+    def _side_stream(self, dev):
+        if not self.overlap_text:
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=dev)
+        return self._side
 
     def _img_bucket_hook(self):
         """Launch the all-reduce of image layers [li, prev) every bucket_layers layers."""
