@@ -40,6 +40,14 @@ def _key(*tensors):
     return tuple((t.data_ptr(), t._version) for t in tensors if t is not None)
 
 
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class StagedBlock:
     """bf16 device copies of one block's GEMM weights (both layouts)."""
 
@@ -192,11 +200,20 @@ class BlockStack:
         return x, saved
 
     # ------------------------------------------------------------------ backward
-    def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None):
+    def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None,
+                 grad_stream=None):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
         param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
-        have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input."""
+        have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input.
+
+        grad_stream: optional side HIP stream for the PEFT weight-gradient reductions (adapter
+        dW/db, LoRA dA/dB), which feed only `grads`: they run beside the dX chain's MFMA-bound
+        GEMMs. Each layer waits for the previous layer's side work before rewriting the shared
+        gradient buffers the side reads; sync_grads() joins it (done before returning)."""
         M, D = dx.shape
+        main = torch.cuda.current_stream(dx.device)
+        self._gs = grad_stream
+        ev = None
         H = self.n_head
         dev = dx.device
         da = _empty((M, 4 * D), BF16, dev)
@@ -210,6 +227,8 @@ class BlockStack:
         dxb_new = _empty((M, D), BF16, dev)
         for li in range(len(self.blocks) - 1, -1, -1):
             blk, st, s = self.blocks[li], self.staged[li], saved[li]
+            if ev is not None:
+                main.wait_event(ev)  # side reads of the buffers this layer rewrites are done
             # ---- MLP sub-block: x_out = x_mid + [A](c_proj(gelu(c_fc(ln_2(x_mid)))))
             if self.variant == "adapter":
                 dY = self._adapter_bwd(blk, st, dxb, s["hd2"], s["z2"], s["keep"], dz, grads)
@@ -236,12 +255,31 @@ class BlockStack:
                                 attn.in_proj_weight_lora_B, attn.scaling, grads)
             ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
                               dxb_new, dres=dx_mid)
+            if grad_stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(grad_stream)
             if on_layer is not None:
                 on_layer(li)
             # ping-pong: the consumed output-gradient buffers are recycled for the next layer
             dx, dx_new = dx_new, dx
             dxb, dxb_new = dxb_new, dxb
+        self.sync_grads()
         return dx, dxb
+
+    def sync_grads(self):
+        """Make the current stream wait for the PEFT-gradient work on the side stream."""
+        gs = getattr(self, "_gs", None)
+        if gs is not None:
+            torch.cuda.current_stream(gs.device).wait_stream(gs)
+
+    def _side(self):
+        """Context for launching gradient reductions: the side stream (after the work that
+        produced their inputs on the current stream) or the current stream."""
+        gs = getattr(self, "_gs", None)
+        if gs is None:
+            return _Null()
+        gs.wait_stream(torch.cuda.current_stream(gs.device))
+        return torch.cuda.stream(gs)
 
     @staticmethod
     def _grad(grads, p):
@@ -255,15 +293,19 @@ class BlockStack:
         M = gout.shape[0]
         dpre = _empty((M, ad.down_size), BF16, gout.device)
         ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz)
-        ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale,
-                    colsum=self._grad(grads, ad.up_proj.bias), colsum_scale=ad.scale)
-        ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0,
-                    colsum=self._grad(grads, ad.down_proj.bias), colsum_scale=1.0)
+        with self._side():
+            if getattr(self, "_gs", None) is not None:
+                dpre.record_stream(self._gs)
+            ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale,
+                        colsum=self._grad(grads, ad.up_proj.bias), colsum_scale=ad.scale)
+            ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0,
+                        colsum=self._grad(grads, ad.down_proj.bias), colsum_scale=1.0)
         return dz
 
     def _lora_grad(self, dY, X, A, B, scaling, grads):
-        ops.lora_grad(dY, X, A.detach(), B.detach(), scaling, self._grad(grads, A),
-                      self._grad(grads, B))
+        with self._side():
+            ops.lora_grad(dY, X, A.detach(), B.detach(), scaling, self._grad(grads, A),
+                          self._grad(grads, B))
 
 
 class ImageTower:
@@ -318,7 +360,7 @@ class ImageTower:
         ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads, on_layer=None):
+    def backward(self, ctx, df, grads, on_layer=None, grad_stream=None):
         v = self.visual
         dev = df.device
         n, L = ctx["n"], ctx["L"]
@@ -331,7 +373,7 @@ class ImageTower:
         dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer)
+        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream)
 
 
 class TextTower:

@@ -43,7 +43,7 @@ def remap_labels(labels, class_list=None):
 class OnlineTrainer:
     def __init__(self, adapter_clip, lr=5e-4, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  process_group=None, distributed=None, shard_text=True, bucket_layers=4,
-                 overlap_text=True):
+                 overlap_text=True, overlap_grads=True):
         self.wrapper = adapter_clip
         self.clip = adapter_clip.model
         freeze_backbone(self.wrapper)
@@ -80,7 +80,9 @@ class OnlineTrainer:
         self.step_count = 0
         self.graph = None
         self.overlap_text = bool(overlap_text)
+        self.overlap_grads = bool(overlap_grads)
         self._side = None
+        self._gstream = None
         self.logit_scale = self.clip.logit_scale.detach().reshape(1)
 
     def reset_optimizer(self):
@@ -140,11 +142,19 @@ class OnlineTrainer:
                     w_dt.wait()  # makes the text stream wait for the dL/dT all-reduce
                 self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
         if self.img.stack.trainable_params():
-            self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook())
+            self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook(),
+                              grad_stream=self._grad_stream(dev))
         if side is not None:
             main.wait_stream(side)
         dp.launch_bucket(self.flat_g, *self.txt_range)
         return loss, probs
+
+    def _grad_stream(self, dev):
+        if not self.overlap_grads:
+            return None
+        if self._gstream is None:
+            self._gstream = torch.cuda.Stream(device=dev)
+        return self._gstream
 
     def _side_stream(self, dev):
         if not self.overlap_text:
@@ -161,6 +171,7 @@ class OnlineTrainer:
 
         def hook(li):
             if li % self.bucket_layers == 0:
+                self.img.stack.sync_grads()  # the bucket's gradients are complete
                 lo_r = self.img_ranges[li][0]
                 hi_r = self.img_ranges[state["hi"] - 1][1]
                 self.dp.launch_bucket(self.flat_g, lo_r, hi_r)
