@@ -61,6 +61,9 @@ int lc_gemm_set_debug(unsigned long long* p);
 
 /* C[N1,N2] += alpha * A[M,N1]^T . B[M,N2] (f32 C, atomically accumulated; split over M);
  * if colsum != NULL also colsum[N1] += colsum_scale * sum_m A[m][:] (the bias gradient).
+ * A and B rows are read in 64-column blocks: lda >= N1 and ldb >= N2 rounded up to 64 (the
+ * padding columns are read, their products masked) — this is how the rank-4 LoRA gradients
+ * run on it with zero-padded [M,64] operands.
  * Replaces: the autograd weight- and bias-gradient reductions of adapter down_proj / up_proj
  * (models/clip/adapter.py:38-40, 59-62). */
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,

@@ -460,7 +460,7 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
   float* red = reinterpret_cast<float*>(smem + 2 * 2 * TN_BM * 128);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wa = wave >> 1, wb = wave & 1;
-  const int tiles_n2 = N2 / 64;
+  const int tiles_n2 = (N2 + 63) / 64;
   const int t1 = blockIdx.x / tiles_n2, t2 = blockIdx.x % tiles_n2;
   const int c1 = t1 * 64, c2 = t2 * 64;
   const int mbeg = blockIdx.y * chunk_rows;
@@ -540,7 +540,8 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
   if (do_cs) {
     red[tid] = cs;
     __syncthreads();
-    if (tid < 64) atomicAdd(colsum + c1 + tid, colsum_scale * (red[tid] + red[tid + 64] + red[tid + 128] + red[tid + 192]));
+    if (tid < 64 && c1 + tid < N1)
+      atomicAdd(colsum + c1 + tid, colsum_scale * (red[tid] + red[tid + 64] + red[tid + 128] + red[tid + 192]));
   }
   // acc[i][j]: lane holds D[n1 = 4g + r][n2 = t] of subtile (i, j)
   const int g = lane >> 4, t = lane & 15;
@@ -552,7 +553,7 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
       for (int r = 0; r < 4; ++r) {
         const int n1 = c1 + wa * 32 + i * 16 + g * 4 + r;
         const int n2 = c2 + wb * 32 + j * 16 + t;
-        atomicAdd(C + (long)n1 * ldc + n2, acc[i][j][r] * alpha);
+        if (n1 < N1 && n2 < N2) atomicAdd(C + (long)n1 * ldc + n2, acc[i][j][r] * alpha);
       }
 }
 
@@ -701,9 +702,12 @@ int lc_gemm_set_tile(int tile) {
 
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
                long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale) {
-  LC_CHECK_ARG(M > 0 && N1 % 64 == 0 && N2 % 64 == 0 && N1 > 0 && N2 > 0);
-  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= N1 && ldb >= N2 && ldc >= N2);
-  const int tiles = (N1 / 64) * (N2 / 64);
+  LC_CHECK_ARG(M > 0 && N1 > 0 && N2 > 0);
+  // operand rows are read in 64-column blocks: they must be readable up to the next multiple
+  // of 64 (zero padding); outputs beyond N1 x N2 are masked
+  LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= (N1 + 63) / 64 * 64 &&
+               ldb >= (N2 + 63) / 64 * 64 && ldc >= N2);
+  const int tiles = ((N1 + 63) / 64) * ((N2 + 63) / 64);
   // Enough M-chunks to give ~4 workgroups per CU, each chunk a multiple of 64 rows.
   int splits = (1024 + tiles - 1) / tiles;
   int chunk = (M + splits - 1) / splits;

@@ -120,6 +120,11 @@ class BlockStack:
                                      attn.in_proj_weight_lora_B.detach(), s, st.wqkv, st.wqkvT)
                     ops.merge_weight(attn.out_proj.weight.detach(), attn.out_proj.lora_A.detach(),
                                      attn.out_proj.lora_B.detach(), s, st.wo, st.woT)
+                    # bf16 A and B^T zero-padded to 64 rows: operands of the LoRA-gradient GEMMs
+                    st.lora_in = self._stage_lora(st, "lora_in", attn.in_proj_weight_lora_A,
+                                                  attn.in_proj_weight_lora_B)
+                    st.lora_out = self._stage_lora(st, "lora_out", attn.out_proj.lora_A,
+                                                   attn.out_proj.lora_B)
                     st.peft_key = pkey
             elif self.variant == "adapter":
                 ad = blk.adaptmlp
@@ -135,6 +140,22 @@ class BlockStack:
                     ops.merge_weight(ad.down_proj.weight.detach(), None, None, 0.0, st.wd, st.wdT)
                     ops.merge_weight(ad.up_proj.weight.detach(), None, None, 0.0, st.wu, st.wuT)
                     st.peft_key = pkey
+
+    @staticmethod
+    def _stage_lora(st, name, A, B):
+        """(A_pad [64,K], Bt_pad [64,N]) bf16 with rows >= r zero, staged from A [r,K], B [N,r]."""
+        r, K = A.shape
+        N = B.shape[0]
+        old = getattr(st, name, None)
+        dev = A.device
+        if old is None or old[0].shape[1] != K or old[1].shape[1] != N:
+            old = (torch.zeros((64, K), dtype=BF16, device=dev),
+                   torch.zeros((64, N), dtype=BF16, device=dev),
+                   _empty((N, r), BF16, dev))
+        a_pad, bt_pad, scratch = old
+        ops.merge_weight(A.detach(), None, None, 0.0, a_pad[:r])
+        ops.merge_weight(B.detach(), None, None, 0.0, scratch, bt_pad[:r])
+        return old
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False):
@@ -247,12 +268,12 @@ class BlockStack:
             attn = blk.attn
             if self.variant == "lora":
                 self._lora_grad(dY, s["O"], attn.out_proj.lora_A, attn.out_proj.lora_B,
-                                attn.scaling, grads)
+                                attn.scaling, grads, st.lora_out)
             ops.attn_bwd(s["qkv"], s["O"], dO, s["lse"], dqkv, n_seq, L, H, self.causal)
             ops.gemm_nt(dqkv, st.wqkvT, EPI_BF16, dh)
             if self.variant == "lora":
                 self._lora_grad(dqkv, s["h1"], attn.in_proj_weight_lora_A,
-                                attn.in_proj_weight_lora_B, attn.scaling, grads)
+                                attn.in_proj_weight_lora_B, attn.scaling, grads, st.lora_in)
             ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
                               dxb_new, dres=dx_mid)
             if grad_stream is not None:
@@ -302,10 +323,23 @@ class BlockStack:
                         colsum=self._grad(grads, ad.down_proj.bias), colsum_scale=1.0)
         return dz
 
-    def _lora_grad(self, dY, X, A, B, scaling, grads):
+    def _lora_grad(self, dY, X, A, B, scaling, grads, padded):
+        """Rank-r LoRA gradients (lora.py:838-839, 1073-1074 autograd) as four streaming GEMMs:
+        XA = X A^T and dYB = dY B (skinny, [M,64] bf16 with zero columns >= r), then
+        dB += s dY^T XA and dA += s dYB^T X (gemm_tn, outputs masked to r)."""
+        a_pad, bt_pad, _ = padded
+        M = dY.shape[0]
         with self._side():
-            ops.lora_grad(dY, X, A.detach(), B.detach(), scaling, self._grad(grads, A),
-                          self._grad(grads, B))
+            xa = _empty((M, 64), BF16, dY.device)
+            dyb = _empty((M, 64), BF16, dY.device)
+            gs = getattr(self, "_gs", None)
+            if gs is not None:
+                xa.record_stream(gs)
+                dyb.record_stream(gs)
+            ops.gemm_nt(X, a_pad, EPI_BF16, xa)
+            ops.gemm_nt(dY, bt_pad, EPI_BF16, dyb)
+            ops.gemm_tn(dY, xa, self._grad(grads, B), alpha=scaling)
+            ops.gemm_tn(dyb, X, self._grad(grads, A), alpha=scaling)
 
 
 class ImageTower:

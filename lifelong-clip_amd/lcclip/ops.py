@@ -37,14 +37,18 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
 
 
 def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
-    """C[N1,N2] += alpha * A[M,N1]^T @ B[M,N2] (C f32); colsum[N1] += colsum_scale * sum_m A."""
+    """C[N1,N2] += alpha * A[M,:N1]^T @ B[M,:N2] (C f32, N1 x N2 = C's shape); colsum[N1] +=
+    colsum_scale * sum_m A[:, :N1]. A / B may be wider than N1 / N2 (zero padding to 64)."""
     _rowmajor(A, BF16, "A")
     _rowmajor(B, BF16, "B")
     _rowmajor(C, F32, "C")
-    M, N1 = A.shape
-    N2 = B.shape[1]
-    if B.shape[0] != M or C.shape[0] != N1 or C.shape[1] != N2:
-        raise ValueError("gemm_tn shape mismatch")
+    M = A.shape[0]
+    N1, N2 = C.shape
+    pad = lambda n: (n + 63) // 64 * 64  # noqa: E731
+    # the kernel reads whole 64-column blocks of every row, the last row included
+    if B.shape[0] != M or A.shape[1] < pad(N1) or B.shape[1] < pad(N2):
+        raise ValueError("gemm_tn shape mismatch (operands must be readable to 64-column "
+                         "multiples of C's shape)")
     if colsum is not None and (colsum.dtype != F32 or colsum.numel() != N1):
         raise ValueError("colsum must be f32 [N1]")
     call("lc_gemm_tn", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),

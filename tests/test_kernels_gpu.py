@@ -93,6 +93,22 @@ def test_gemm_tn(ops, dev, M, N1, N2):
     assert rel(cs - 1, 0.25 * A.float().sum(0)) < 1e-5
 
 
+def test_gemm_tn_masked_rank4(ops, dev):
+    """N1 or N2 below 64 (zero-padded [M,64] operands, outputs masked): the LoRA dA / dB path."""
+    torch.manual_seed(11)
+    M, N, r = 3000, 2304, 4
+    dY = torch.randn(M, N, device=dev).to(BF)
+    xa = torch.zeros(M, 64, device=dev, dtype=BF)
+    xa[:, :r] = torch.randn(M, r, device=dev).to(BF)
+    dB = torch.ones(N, r, device=dev)
+    ops.gemm_tn(dY, xa, dB, alpha=0.25)
+    assert rel(dB - 1, 0.25 * dY.float().t() @ xa[:, :r].float()) < 1e-5
+    X = torch.randn(M, 768, device=dev).to(BF)
+    dA = torch.zeros(r, 768, device=dev)
+    ops.gemm_tn(xa, X, dA, alpha=2.0)
+    assert rel(dA, 2.0 * xa[:, :r].float().t() @ X.float()) < 1e-5
+
+
 # ------------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("D", [64, 128, 512, 768])
 def test_layernorm_fwd_bwd(ops, dev, D):
