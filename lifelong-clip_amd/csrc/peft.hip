@@ -26,30 +26,80 @@ __global__ void cast_bf16_kernel(long n, const float* __restrict__ src, bf16_t* 
   }
 }
 
-// dst (+)= bf16 of W[N,K] + s*B[N,r]@A[r,K] in [N,K] layout and optionally [K,N].
-// 64x64 tiles through LDS so the transposed write is coalesced.
-__global__ void merge_kernel(int N, int K, int r, const float* __restrict__ W,
-                             const float* __restrict__ A, const float* __restrict__ B, float s,
-                             bf16_t* __restrict__ out, bf16_t* __restrict__ outT) {
+// out = bf16(W[N,K] + s * B[N,r] @ A[r,K]) in [N,K] layout and optionally outT in [K,N].
+// 64x64 tile per 256-thread workgroup: the r rows of A and r columns of B for the tile staged in
+// LDS once, each thread 4 rows x 4 columns (float4 loads of W, 8-byte bf16 stores), and the
+// transposed copy written from an LDS tile as 4 consecutive columns per store.
+constexpr int MERGE_RMAX = 8;
+__global__ void __launch_bounds__(256)
+merge_kernel(int N, int K, int r, const float* __restrict__ W, const float* __restrict__ A,
+             const float* __restrict__ B, float s, bf16_t* __restrict__ out,
+             bf16_t* __restrict__ outT) {
   __shared__ float tile[64][65];
+  __shared__ float As[MERGE_RMAX][64];
+  __shared__ float Bs[64][MERGE_RMAX];
+  const int tid = threadIdx.x;
   const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
-  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
-    const int nn = i / 64, kk = i % 64;
-    const int n = n0 + nn, k = k0 + kk;
-    float v = 0.f;
-    if (n < N && k < K) {
-      v = W[(long)n * K + k];
-      for (int j = 0; j < r; ++j) v += s * B[n * r + j] * A[(long)j * K + k];
-      out[(long)n * K + k] = f2bf(v);
+  for (int i = tid; i < r * 64; i += 256) {
+    const int j = i / 64, kk = i % 64;
+    As[j][kk] = (k0 + kk < K) ? A[(long)j * K + k0 + kk] : 0.f;
+  }
+  for (int i = tid; i < 64 * r; i += 256) {
+    const int nn = i / r, j = i % r;
+    Bs[nn][j] = (n0 + nn < N) ? B[(long)(n0 + nn) * r + j] : 0.f;
+  }
+  if (r > 0) __syncthreads();
+  const int nn0 = (tid >> 4) * 4, kk0 = (tid & 15) * 4;
+  const int kb = k0 + kk0;
+  const bool vec = (K % 4 == 0) && (kb + 3 < K);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int nn = nn0 + rr, n = n0 + nn;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (n < N) {
+      if (vec) {
+        const float4 w = *reinterpret_cast<const float4*>(W + (long)n * K + kb);
+        v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = (kb + c < K) ? W[(long)n * K + kb + c] : 0.f;
+      }
+      for (int j = 0; j < r; ++j) {
+        const float bj = s * Bs[nn][j];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] += bj * As[j][kk0 + c];
+      }
+      if (vec) {
+        *reinterpret_cast<uint2*>(out + (long)n * K + kb) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (kb + c < K) out[(long)n * K + kb + c] = f2bf(v[c]);
+      }
     }
-    tile[nn][kk] = v;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) tile[nn][kk0 + c] = v[c];
   }
   if (!outT) return;
   __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
-    const int kk = i / 64, nn = i % 64;
-    const int n = n0 + nn, k = k0 + kk;
-    if (n < N && k < K) outT[(long)k * N + n] = f2bf(tile[nn][kk]);
+  // transposed: thread -> 4 k rows x 4 consecutive n
+  const int kt0 = (tid >> 4) * 4, nt0 = (tid & 15) * 4;
+  const int nb = n0 + nt0;
+  const bool vecT = (N % 4 == 0) && (nb + 3 < N);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int k = k0 + kt0 + rr;
+    if (k >= K) continue;
+    const float* tcol = &tile[0][kt0 + rr];
+    if (vecT) {
+      *reinterpret_cast<uint2*>(outT + (long)k * N + nb) =
+          uint2{pack2bf(tcol[(nt0 + 0) * 65], tcol[(nt0 + 1) * 65]),
+                pack2bf(tcol[(nt0 + 2) * 65], tcol[(nt0 + 3) * 65])};
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (nb + c < N) outT[(long)k * N + nb + c] = f2bf(tcol[(nt0 + c) * 65]);
+    }
   }
 }
 
@@ -240,7 +290,7 @@ int lc_cast_bf16(hipStream_t st, long n, const float* src, void* dst) {
 
 int lc_merge_weight(hipStream_t st, int N, int K, int r, const float* W, const float* A,
                     const float* B, float scaling, void* out, void* outT) {
-  LC_CHECK_ARG(N > 0 && K > 0 && r >= 0 && (r == 0 || (A && B)));
+  LC_CHECK_ARG(N > 0 && K > 0 && r >= 0 && r <= MERGE_RMAX && (r == 0 || (A && B)));
   dim3 grid((K + 63) / 64, (N + 63) / 64);
   hipLaunchKernelGGL(merge_kernel, grid, dim3(256), 0, st, N, K, r, W, A, B, scaling,
                      (bf16_t*)out, (bf16_t*)outT);

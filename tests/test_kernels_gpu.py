@@ -237,6 +237,15 @@ def test_lora_merge_and_grad(ops, dev):
     ref = W + 0.25 * B @ A
     assert rel(out, ref) < 4e-3
     assert torch.equal(outT, out.t())
+    # ragged shapes (edge tiles, scalar paths) and the padded-operand staging uses (r = 0)
+    for n_, k_, r_ in [(100, 70, 4), (2304, 4, 0), (4, 768, 0), (77, 131, 3)]:
+        W2 = torch.randn(n_, k_, device=dev)
+        A2, B2 = torch.randn(r_, k_, device=dev), torch.randn(n_, r_, device=dev)
+        o2 = torch.empty(n_, k_, device=dev, dtype=BF)
+        o2T = torch.empty(k_, n_, device=dev, dtype=BF)
+        ops.merge_weight(W2, A2 if r_ else None, B2 if r_ else None, 0.5, o2, o2T)
+        assert rel(o2, W2 + 0.5 * B2 @ A2) < 4e-3
+        assert torch.equal(o2T, o2.t())
     dY = torch.randn(M, N, device=dev).to(BF)
     X = torch.randn(M, K, device=dev).to(BF)
     dA = torch.zeros(r, K, device=dev)
