@@ -90,16 +90,30 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   constexpr int WT_M = BM / WM, WT_N = BN / WN;
   constexpr int PASS = (WT_M % 32 == 0) ? 32 : 16;
   constexpr int LSTR = WT_N + 4;          // floats per staged row (pad: bank spread)
-  constexpr int LPR = WT_N / 4;           // lanes per row (4 columns each)
+  // columns per lane on the read-back: 8 when every output is bf16 (one 16-B store per lane and
+  // output: half the store instructions of 4 columns — the epilogue tail is store-issue bound),
+  // 4 when an output is f32 (already 16 B per lane)
+  constexpr bool F32OUT = (EPI == EPI_F32 || EPI == EPI_RESID || EPI == EPI_BF16_F32 ||
+                           EPI == EPI_AD_UP);
+  constexpr int CPL = F32OUT ? 4 : 8;
+  constexpr int NQ = CPL / 4;             // float4 groups per lane
+  constexpr int LPR = WT_N / CPL;         // lanes per row
   constexpr int RPI = 64 / LPR;           // rows per read-back instruction
   (void)smem_bytes;
   float* stg = reinterpret_cast<float*>(smem) + wave * PASS * LSTR;
-  const int lc = (lane % LPR) * 4;
+  const int lc = (lane % LPR) * CPL;
   const int n = n0 + wn * WT_N + lc;
-  float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+  float bb[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) bb[q] = 0.f;
   if (EPI != EPI_GELU_BWD && EPI != EPI_MUL && EPI != EPI_AD_MASK && EPI != EPI_AD_ADD &&
-      bias != nullptr)
-    bb = *reinterpret_cast<const float4*>(bias + n);
+      bias != nullptr) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float4 b4 = *reinterpret_cast<const float4*>(bias + n + 4 * q);
+      bb[4 * q] = b4.x, bb[4 * q + 1] = b4.y, bb[4 * q + 2] = b4.z, bb[4 * q + 3] = b4.w;
+    }
+  }
   // side inputs (residual / pre-activation / adapter z / h) of a pass are fetched one pass
   // ahead, before the stores of the current pass: CDNA's vmcnt also counts stores, so a load
   // issued after them would wait for their acknowledgement.
@@ -108,18 +122,51 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
                          EPI == EPI_AD_ADD);
   constexpr bool AUX2 = (EPI == EPI_AD_UP);
   constexpr int NIT = PASS / RPI;
-  float4 pf_f[2][NIT];
-  uint2 pf_b[2][NIT];
+  float pf_f[2][NIT][CPL];
+  uint32_t pf_b[2][NIT][CPL / 2];
   auto prefetch = [&](int pass, int slot) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       long m = m0 + wm * WT_M + pass * PASS + it * RPI + lane / LPR;
       m = m < M ? m : M - 1;
-      if constexpr (AUXF) pf_f[slot][it] = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n);
-      if constexpr (AUXB) pf_b[slot][it] = *reinterpret_cast<const uint2*>((const bf16_t*)aux + m * ldaux + n);
-      if constexpr (AUX2) pf_b[slot][it] = *reinterpret_cast<const uint2*>((const bf16_t*)ep.aux2 + m * ep.ldaux2 + n);
+      if constexpr (AUXF) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float4 f = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n + 4 * q);
+          pf_f[slot][it][4 * q] = f.x, pf_f[slot][it][4 * q + 1] = f.y;
+          pf_f[slot][it][4 * q + 2] = f.z, pf_f[slot][it][4 * q + 3] = f.w;
+        }
+      }
+      if constexpr (AUXB || AUX2) {
+        const bf16_t* bsrc = AUXB ? (const bf16_t*)aux + m * ldaux + n
+                                  : (const bf16_t*)ep.aux2 + m * ep.ldaux2 + n;
+        if constexpr (CPL == 8) {
+          const uint4 u = *reinterpret_cast<const uint4*>(bsrc);
+          pf_b[slot][it][0] = u.x, pf_b[slot][it][1] = u.y, pf_b[slot][it][2] = u.z, pf_b[slot][it][3] = u.w;
+        } else {
+          const uint2 u = *reinterpret_cast<const uint2*>(bsrc);
+          pf_b[slot][it][0] = u.x, pf_b[slot][it][1] = u.y;
+        }
+      }
     }
   };
+  // one lane's CPL outputs of row m: a single 8-B / 16-B bf16 store, or NQ 16-B f32 stores
+  auto store_bf = [&](void* base, long ld, long m, const float (&w)[CPL]) {
+    bf16_t* p = (bf16_t*)base + m * ld + n;
+    if constexpr (CPL == 8)
+      *reinterpret_cast<uint4*>(p) = uint4{pack2bf(w[0], w[1]), pack2bf(w[2], w[3]),
+                                           pack2bf(w[4], w[5]), pack2bf(w[6], w[7])};
+    else
+      *reinterpret_cast<uint2*>(p) = uint2{pack2bf(w[0], w[1]), pack2bf(w[2], w[3])};
+  };
+  auto store_f = [&](void* base, long ld, long m, const float (&w)[CPL]) {
+    float* p = (float*)base + m * ld + n;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      *reinterpret_cast<float4*>(p + 4 * q) = make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  };
+  // bf16 element i of a lane's packed side input
+  auto bfv = [](const uint32_t* x, int i) { return bf2f((i & 1) ? (x[i >> 1] >> 16) : (x[i >> 1] & 0xffff)); };
   if constexpr (AUXF || AUXB) prefetch(0, 0);
   uint64_t seed = ep.seed;
   if constexpr (EPI == EPI_AD_DOWN)
@@ -138,77 +185,65 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
     for (int it = 0; it < NIT; ++it) {
       const int lr = it * RPI + lane / LPR;
       const long m = m0 + wm * WT_M + pass * PASS + lr;
-      const f32x4 a4 = *reinterpret_cast<const f32x4*>(stg + lr * LSTR + lc);
-      const float4 xf = pf_f[pass & 1][it];
-      const uint2 xb = pf_b[pass & 1][it];
-      if (m >= M) continue;
-      float v[4] = {a4[0] * alpha + bb.x, a4[1] * alpha + bb.y, a4[2] * alpha + bb.z,
-                    a4[3] * alpha + bb.w};
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        if constexpr (EPI == EPI_BF16_F32)
-          *reinterpret_cast<float4*>((float*)out1 + m * ldo1 + n) = make_float4(v[0], v[1], v[2], v[3]);
-      } else if constexpr (EPI == EPI_F32) {
-        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) = make_float4(v[0], v[1], v[2], v[3]);
-      } else if constexpr (EPI == EPI_RESID) {
-        const float4 x = xf;
-        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) =
-            make_float4(x.x + v[0], x.y + v[1], x.z + v[2], x.w + v[3]);
-      } else if constexpr (EPI == EPI_GELU) {
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) =
-            uint2{pack2bf(quick_gelu(v[0]), quick_gelu(v[1])), pack2bf(quick_gelu(v[2]), quick_gelu(v[3]))};
-      } else if constexpr (EPI == EPI_GELU_BWD) {
-        const uint2 a = xb;
-        const float g0 = quick_gelu_grad(bf2f(a.x & 0xffff)), g1 = quick_gelu_grad(bf2f(a.x >> 16));
-        const float g2 = quick_gelu_grad(bf2f(a.y & 0xffff)), g3 = quick_gelu_grad(bf2f(a.y >> 16));
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0] * g0, v[1] * g1), pack2bf(v[2] * g2, v[3] * g3)};
-      } else if constexpr (EPI == EPI_GELU_D) {
-        float gg[4], dd[4];
+      float v[CPL];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float sg = lc_sigmoid1702(v[r]);
-          gg[r] = v[r] * sg;
-          dd[r] = sg * __builtin_fmaf(1.702f * v[r], 1.0f - sg, 1.0f);
+      for (int q = 0; q < NQ; ++q) {
+        const f32x4 a4 = *reinterpret_cast<const f32x4*>(stg + lr * LSTR + lc + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[4 * q + r] = a4[r] * alpha + bb[4 * q + r];
+      }
+      const float* xf = pf_f[pass & 1][it];
+      const uint32_t* xb = pf_b[pass & 1][it];
+      if (m >= M) continue;
+      float w[CPL];
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
+        store_bf(out0, ldo0, m, v);
+        if constexpr (EPI == EPI_BF16_F32) store_f(out1, ldo1, m, v);
+      } else if constexpr (EPI == EPI_F32) {
+        store_f(out0, ldo0, m, v);
+      } else if constexpr (EPI == EPI_RESID) {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = xf[i] + v[i];
+        store_f(out0, ldo0, m, w);
+      } else if constexpr (EPI == EPI_GELU) {
+        store_bf(out0, ldo0, m, v);
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = quick_gelu(v[i]);
+        store_bf(out1, ldo1, m, w);
+      } else if constexpr (EPI == EPI_GELU_BWD) {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = v[i] * quick_gelu_grad(bfv(xb, i));
+        store_bf(out0, ldo0, m, w);
+      } else if constexpr (EPI == EPI_GELU_D) {
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) {
+          const float sg = lc_sigmoid1702(v[i]);
+          w[i] = v[i] * sg;                                            // QuickGELU
+          v[i] = sg * __builtin_fmaf(1.702f * v[i], 1.0f - sg, 1.0f);  // QuickGELU'
         }
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(dd[0], dd[1]), pack2bf(dd[2], dd[3])};
-        *reinterpret_cast<uint2*>((bf16_t*)out1 + m * ldo1 + n) =
-            uint2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])};
+        store_bf(out0, ldo0, m, v);
+        store_bf(out1, ldo1, m, w);
       } else if constexpr (EPI == EPI_MUL) {
-        const uint2 a = xb;
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0] * bf2f(a.x & 0xffff), v[1] * bf2f(a.x >> 16)),
-                  pack2bf(v[2] * bf2f(a.y & 0xffff), v[3] * bf2f(a.y >> 16))};
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = v[i] * bfv(xb, i);
+        store_bf(out0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_DOWN) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f) * drop_mul(seed, m, n + r, ep.keep);
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        for (int i = 0; i < CPL; ++i) w[i] = fmaxf(v[i], 0.f) * drop_mul(seed, m, n + i, ep.keep);
+        store_bf(out0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_UP) {
-        const float4 x = xf;
-        const uint2 zz = xb;
-        *reinterpret_cast<float4*>((float*)out0 + m * ldo0 + n) =
-            make_float4(x.x + bf2f(zz.x & 0xffff) + ep.scale * v[0],
-                        x.y + bf2f(zz.x >> 16) + ep.scale * v[1],
-                        x.z + bf2f(zz.y & 0xffff) + ep.scale * v[2],
-                        x.w + bf2f(zz.y >> 16) + ep.scale * v[3]);
-      } else if constexpr (EPI == EPI_AD_MASK) {
-        const uint2 hv = xb;
-        const float inv = 1.0f / ep.keep;
-        const float hh[4] = {bf2f(hv.x & 0xffff), bf2f(hv.x >> 16), bf2f(hv.y & 0xffff), bf2f(hv.y >> 16)};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = hh[r] > 0.f ? v[r] * inv : 0.f;
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        for (int i = 0; i < CPL; ++i) w[i] = xf[i] + bfv(xb, i) + ep.scale * v[i];
+        store_f(out0, ldo0, m, w);
+      } else if constexpr (EPI == EPI_AD_MASK) {
+        const float inv = 1.0f / ep.keep;
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = bfv(xb, i) > 0.f ? v[i] * inv : 0.f;
+        store_bf(out0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_ADD) {
-        const uint2 gg = xb;
-        *reinterpret_cast<uint2*>((bf16_t*)out0 + m * ldo0 + n) =
-            uint2{pack2bf(bf2f(gg.x & 0xffff) + v[0], bf2f(gg.x >> 16) + v[1]),
-                  pack2bf(bf2f(gg.y & 0xffff) + v[2], bf2f(gg.y >> 16) + v[3])};
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = bfv(xb, i) + v[i];
+        store_bf(out0, ldo0, m, w);
       }
     }
   }
@@ -634,13 +669,14 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
                   void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep) {
   LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
-  LC_CHECK_ARG(ldo0 % 4 == 0 && ldo0 >= N);
+  // epilogue rows are written / side inputs read 8 elements (16 B of bf16) per lane
+  LC_CHECK_ARG(ldo0 % 8 == 0 && ldo0 >= N);
   LC_CHECK_ARG(epi >= 0 && epi <= EPI_AD_ADD);
   if (epi == EPI_GELU || epi == EPI_BF16_F32 || epi == EPI_GELU_D)
-    LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 4 == 0);
+    LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
   if (epi == EPI_RESID || epi == EPI_GELU_BWD || epi == EPI_MUL || epi >= EPI_AD_UP)
-    LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 4 == 0);
-  if (epi == EPI_AD_UP) LC_CHECK_ARG(ep.aux2 != nullptr && ep.ldaux2 >= N && ep.ldaux2 % 4 == 0);
+    LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
+  if (epi == EPI_AD_UP) LC_CHECK_ARG(ep.aux2 != nullptr && ep.ldaux2 >= N && ep.ldaux2 % 8 == 0);
   auto a = static_cast<const bf16_t*>(A);
   auto b = static_cast<const bf16_t*>(B);
   if (g_force_tile < 0) {

@@ -335,7 +335,7 @@ int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const 
 int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, const void* h,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
                    void* dz, long ldz) {
-  LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 4 == 0);
+  LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
   EpiParams ep{nullptr, 0, scale, keep, 0, nullptr};
   int rc = lc_gemm_nt_ex(st, 10 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
