@@ -49,6 +49,19 @@ int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, 
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux);
 
+/* lc_gemm_nt with a caller-owned workspace for the split-K tail: when the 256x256 tiles of a
+ * launch leave the last round over the CUs at most half full (e.g. N = 768 at M = 50 432: 591
+ * tiles on 256 CUs), those tiles are cut along K into 2-4 slices whose f32 partial tiles meet in
+ * ws and are summed (in slice order, deterministic) by the last slice before the epilogue.
+ * ws: device memory, 256-B aligned, ws_bytes >= LC_SPLITK_TICKET_BYTES; its first
+ * LC_SPLITK_TICKET_BYTES must be zero before the first use (the kernel leaves them zero), the
+ * rest is scratch (up to 64 MiB is used). ws = NULL is plain lc_gemm_nt. Launches that share a
+ * workspace must be stream-ordered. Same call sites as lc_gemm_nt. */
+#define LC_SPLITK_TICKET_BYTES 16384
+int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                  void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes);
+
 /* Tile-shape override for lc_gemm_nt (tuning): 0 = automatic, 1 = 128x128 (4 waves),
  * 2 = 256x128 (8 waves, 3-stage LDS ring), 3 = 256x256 (8 waves, 2 stages), 4 = 128x64,
  * 5 = 256x256 ping-pong (8 waves in two staggered groups, 4-slot k-half LDS ring), 6 = same.

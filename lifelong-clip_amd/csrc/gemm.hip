@@ -351,12 +351,26 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 // lgkmcnt(0) precedes the barriers in front of LOAD(h) of either group.
 LC_DEV int swz64(int row, int chunk) { return chunk ^ (((row >> 3) & 1) << 1); }
 
+// Split-K tail of the ping-pong GEMM. A launch of T output tiles on C CUs runs ceil(T/C) rounds;
+// when the last round is only partly filled (N = 768 at M = 50 432: 591 tiles = 2.31 rounds),
+// its R = T mod C tiles are instead cut along K into S slices (R*S <= C workgroups, one extra
+// short round). Each slice workgroup writes its f32 accumulators to a slab (register-image
+// layout, 256 KiB per tile slice), publishes with an agent-scope release + ticket atomic; the
+// workgroup that draws the last ticket acquires, adds the other slabs and runs the normal fused
+// epilogue, then resets the ticket (counters start zeroed: the caller's workspace).
+struct SplitK {
+  int dp_tiles;   // tiles [0, dp_tiles) run whole; tiles [dp_tiles, T) are split
+  int splits;     // S (1 = no split-K)
+  float* slabs;   // [(T - dp_tiles) * S][256 * 256] f32
+  int* tickets;   // [T - dp_tiles], zero between launches
+};
+
 template <int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
                const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
                float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
-               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
+               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep, SplitK sk) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 8 x 4 subtiles per wave
   constexpr int SLOT = (BM + BN) * 64;                 // one k-half: 32 KiB
@@ -370,12 +384,20 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;  // wm = group
   const int tiles_n = N / BN;
-  const int tiles_m = (M + BM - 1) / BM;
-  const int nwg = tiles_m * tiles_n;
   int bid = blockIdx.x;
-  {
+  int split = -1;  // >= 0: this workgroup computes K-slice `split` of a tail tile
+  int hb = 0, he = K / 32;  // k-halves [hb, he) of this workgroup
+  if (bid < sk.dp_tiles) {
+    const int nwg = sk.dp_tiles;  // XCD-aware bijective remap over the whole-tile part
     int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  } else {
+    const int s_id = bid - sk.dp_tiles;
+    split = s_id % sk.splits;
+    bid = sk.dp_tiles + s_id / sk.splits;
+    const int nh_all = K / 32;
+    hb = split * nh_all / sk.splits;
+    he = (split + 1) * nh_all / sk.splits;
   }
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -386,7 +408,9 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nh = K / 32;
+  const int nh = he - hb;  // halves of this workgroup; h below counts from 0 (slot = h % 4)
+  const bf16_t* __restrict__ Ak = A + hb * 32;
+  const bf16_t* __restrict__ Bk = B + hb * 32;
   // piece p of this wave = 16-row block p*8 + wave of half h (A blocks 0..15, B blocks 16..31)
   auto dma_piece = [&](int h, int p) {
     const int blk = p * 8 + wave;
@@ -398,7 +422,7 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     const int rows_valid = isA ? M : N;
     int gr = (isA ? m0 : n0) + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
-    const bf16_t* src = isA ? A + (long)gr * lda : B + (long)gr * ldb;
+    const bf16_t* src = isA ? Ak + (long)gr * lda : Bk + (long)gr * ldb;
     glds16(src + h * 32 + c * 8, sl + (isA ? 0 : BM * 64) + b * 1024);
   };
   auto dma_half = [&](int h) {
@@ -470,6 +494,52 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     __builtin_amdgcn_s_barrier();
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
+  if (split >= 0) {
+    // publish this K-slice (G16 recipe: stores drained, barrier, agent release, ticket)
+    const int tail = bid - sk.dp_tiles;
+    constexpr int SLAB = BM * BN;  // floats
+    float* mine = sk.slabs + ((long)tail * sk.splits + split) * SLAB;
+    const int lane_off = (wave * TM * TN * 64 + lane) * 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(mine + lane_off + (i * TN + j) * 256) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(sk.tickets + tail, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const int last = ticket == sk.splits - 1;
+      if (last) {
+        __hip_atomic_store(sk.tickets + tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();  // flag read by every wave before the epilogue reuses the LDS
+    if (!last) return;
+    // sum every slice's slab (own included) in slice order: the result does not depend on
+    // which slice arrived last
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < sk.splits; ++s) {
+      const float* other = sk.slabs + ((long)tail * sk.splits + s) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += *reinterpret_cast<const f32x4*>(other + lane_off + (i * TN + j) * 256);
+    }
+  }
   store_tile<BM, BN, WM, WN, EPI>(acc, smem, NSLOT * SLOT, m0, n0, M, bias, alpha, out0, ldo0,
                                   out1, ldo1, aux, ldaux, ep);
 }
@@ -623,15 +693,58 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
   LC_LAUNCH_RET();
 }
 
+int g_split_mode = -1;  // LC_GEMM_SPLITK=0 disables the split-K tail (A/B experiments)
+
+int cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// Split-K plan for the tail round (see SplitK): S slices of >= 16 k-halves each, R*S <= CUs,
+// only when the last round is at most half full and the workspace holds the slabs.
+SplitK plan_split(int tiles, int K, void* ws, long ws_bytes) {
+  SplitK sk{tiles, 1, nullptr, nullptr};
+  if (g_split_mode < 0) {
+    const char* e = getenv("LC_GEMM_SPLITK");
+    g_split_mode = e ? atoi(e) : 1;
+  }
+  if (!g_split_mode || ws == nullptr) return sk;
+  const int cus = cu_count();
+  const int rem = tiles % cus;
+  if (tiles < cus || rem == 0 || rem > cus / 2) return sk;
+  int S = cus / rem;
+  S = S > 4 ? 4 : S;
+  const int nh = K / 32;
+  if (S > nh / 16) S = nh / 16;  // measured: slices under 16 halves (K = 768) lose
+  if (S < 2) return sk;
+  const long tick_bytes = LC_SPLITK_TICKET_BYTES;
+  if ((long)rem * 4 > tick_bytes || tick_bytes + (long)rem * S * 256 * 256 * 4 > ws_bytes) return sk;
+  sk.dp_tiles = tiles - rem;
+  sk.splits = S;
+  sk.tickets = static_cast<int*>(ws);
+  sk.slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + tick_bytes);
+  return sk;
+}
+
 int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
-              void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep, void* ws,
+              long ws_bytes) {
   const int tiles = ((M + 255) / 256) * (N / 256);
-  dim3 grid(tiles), block(512);
+  const SplitK sk = plan_split(tiles, K, ws, ws_bytes);
+  dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
 #define LC_PP_CASE(E)                                                                          \
   case E:                                                                                      \
     hipLaunchKernelGGL((gemm_pp_kernel<E>), grid, block, 0, st, M, N, K, A, lda, B, ldb, bias, \
-                       alpha, o0, l0, o1, l1, aux, la, ep);                                    \
+                       alpha, o0, l0, o1, l1, aux, la, ep, sk);                                \
     break;
   switch (epi) {
     LC_PP_CASE(EPI_BF16)
@@ -666,7 +779,8 @@ extern "C" {
 
 int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
-                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep) {
+                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep,
+                  void* ws, long ws_bytes) {
   LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
   // epilogue rows are written / side inputs read 8 elements (16 B of bf16) per lane
@@ -706,7 +820,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     case 5:
     case 6:
       return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
-                       aux, ldaux, ep);
+                       aux, ldaux, ep, ws, ws_bytes);
     default:
       return launch_nt<128, 64, 4, 1, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                          ldo0, out1, ldo1, aux, ldaux, ep);
@@ -719,10 +833,18 @@ extern "C" {
 int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                void* out1, long ldo1, const void* aux, long ldaux) {
+  return lc_gemm_nt_ws(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                       aux, ldaux, nullptr, 0);
+}
+
+int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                  const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                  void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes) {
   LC_CHECK_ARG(epi >= 0 && epi <= 7);
+  LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
   EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
   return lc_gemm_nt_ex(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
-                       aux, ldaux, ep);
+                       aux, ldaux, ep, ws, ws_bytes);
 }
 
 int lc_gemm_set_debug(unsigned long long* p) {

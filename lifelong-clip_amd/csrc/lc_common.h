@@ -93,7 +93,8 @@ struct EpiParams {
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).
 int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
-                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep);
+                  void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep,
+                  void* ws = nullptr, long ws_bytes = 0);
 
 #define LC_CHECK_ARG(cond) \
   do {                     \

@@ -20,8 +20,27 @@ def _rowmajor(t, dtype, name):
                          f"strides {t.stride()}")
 
 
+SPLITK_TICKET_BYTES = 16384           # LC_SPLITK_TICKET_BYTES
+SPLITK_WS_BYTES = SPLITK_TICKET_BYTES + 256 * 256 * 256 * 4   # tickets + 256 partial tiles
+_workspaces = {}
+
+
+def splitk_workspace(stream):
+    """The split-K workspace of one HIP stream (launches on a stream are ordered, so they may
+    share it): zeroed tickets + slab scratch, allocated from torch's caching allocator once."""
+    key = (stream.device_index, stream.cuda_stream)
+    ws = _workspaces.get(key)
+    if ws is None:
+        with torch.cuda.stream(stream):
+            ws = torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=stream.device)
+            ws[:SPLITK_TICKET_BYTES].zero_()
+        _workspaces[key] = ws
+    return ws
+
+
 def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
-    """out = epilogue(alpha * A @ B^T + bias); A [M,K] bf16, B [N,K] bf16."""
+    """out = epilogue(alpha * A @ B^T + bias); A [M,K] bf16, B [N,K] bf16. Large launches use
+    the current stream's split-K workspace for their tail round (lc_gemm_nt_ws)."""
     _rowmajor(A, BF16, "A")
     _rowmajor(B, BF16, "B")
     M, K = A.shape
@@ -30,9 +49,12 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
         raise ValueError(f"gemm_nt shapes A{tuple(A.shape)} B{tuple(B.shape)} out{tuple(out0.shape)}")
     if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
         raise ValueError("gemm_nt bias must be a contiguous f32 vector of length N")
-    call("lc_gemm_nt", stream_of(A), epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
+    st = stream_of(A)
+    ws = splitk_workspace(torch.cuda.current_stream(A.device)) if M >= 4096 else None
+    call("lc_gemm_nt_ws", st, epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
          ptr(bias), float(alpha), ptr(out0), out0.stride(0), ptr(out1),
-         out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0)
+         out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
+         ptr(ws), ws.numel() if ws is not None else 0)
     return out0
 
 

@@ -36,6 +36,35 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 5])
+def test_gemm_nt_every_tile_exact(ops, dev, tile):
+    """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
+    the fused QuickGELU-derivative epilogue against torch at bf16 tolerance."""
+    from lcclip import _lib
+    lib = _lib.load()
+    M, N, K = 4096 + 197, 512, 1024
+    g = torch.Generator(device=dev).manual_seed(tile)
+    A = torch.randint(-3, 4, (M, K), device=dev, generator=g).to(BF)
+    B = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(BF)
+    bias = torch.randint(-8, 9, (N,), device=dev, generator=g).float()
+    out = torch.full((M, N), float("nan"), device=dev)
+    gd = torch.empty(M, N, device=dev, dtype=BF)
+    gl = torch.empty(M, N, device=dev, dtype=BF)
+    Ar = torch.randn(M, K, device=dev).to(BF)
+    Br = (torch.randn(N, K, device=dev) * K ** -0.5).to(BF)
+    try:
+        assert lib.lc_gemm_set_tile(tile) == 0
+        ops.gemm_nt(A, B, ops.EPI_F32, out, bias=bias)
+        ops.gemm_nt(Ar, Br, ops.EPI_GELU_D, gd, bias=bias, out1=gl)
+    finally:
+        lib.lc_gemm_set_tile(0)
+    assert torch.equal(out, A.float() @ B.float().t() + bias)
+    pre = Ar.float() @ Br.float().t() + bias
+    s = torch.sigmoid(1.702 * pre)
+    assert rel(gl, pre * s) < 4e-3
+    assert rel(gd, s + 1.702 * pre * s * (1 - s)) < 4e-3
+
+
 @pytest.mark.parametrize("M,N,K", [(1000, 384, 768), (77, 192, 128), (197 * 3, 2304, 768)])
 def test_gemm_nt_epilogues(ops, dev, M, N, K):
     torch.manual_seed(0)
@@ -78,6 +107,42 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
     Aw = torch.randn(M, K + 64, device=dev).to(BF)[:, 64:]
     ops.gemm_nt(Aw, B, ops.EPI_F32, o32)
     assert rel(o32, Aw.float() @ B.float().t()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
+                                   (296 * 256 - 100, 256, 2048)])
+def test_gemm_splitk_tail(ops, dev, M, N, K):
+    """The split-K tail of the 256x256 ping-pong GEMM (lc_gemm_nt_ws): these shapes leave the
+    last round over 256 CUs at most half full (591 / 2364 / 296 tiles), so their tail tiles are
+    summed from 3-4 K-slices. Small integers: every partial sum is exact in f32, so the result
+    must equal torch's bit for bit, for both the split and the plain (ws = NULL) launch; the
+    fused epilogue must see the summed tile exactly once (bias added once)."""
+    from lcclip._lib import call, ptr, stream_of
+    g = torch.Generator(device=dev).manual_seed(7)
+    A = torch.randint(-3, 4, (M, K), device=dev, generator=g).to(BF)
+    B = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(BF)
+    bias = torch.randint(-8, 9, (N,), device=dev, generator=g).float()
+    ref = A.float() @ B.float().t() + bias
+    out = torch.full((M, N), float("nan"), device=dev)
+    ops.gemm_nt(A, B, ops.EPI_F32, out, bias=bias)  # M >= 4096: uses the stream's workspace
+    assert torch.equal(out, ref)
+    out2 = torch.full((M, N), float("nan"), device=dev)
+    call("lc_gemm_nt_ws", stream_of(A), ops.EPI_F32, M, N, K, ptr(A), K, ptr(B), K, ptr(bias),
+         1.0, ptr(out2), N, None, 0, None, 0, None, 0)
+    assert torch.equal(out2, ref)
+    # tickets are left zero for the next launch
+    ws = ops.splitk_workspace(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    assert int(ws[:ops.SPLITK_TICKET_BYTES].sum()) == 0
+    # bf16 epilogue on random data: deterministic across launches
+    Ar = torch.randn(M, K, device=dev).to(BF)
+    Br = (torch.randn(N, K, device=dev) * K ** -0.5).to(BF)
+    o1 = torch.empty(M, N, device=dev, dtype=BF)
+    o2 = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(Ar, Br, ops.EPI_BF16, o1, bias=bias)
+    ops.gemm_nt(Ar, Br, ops.EPI_BF16, o2, bias=bias)
+    assert torch.equal(o1, o2)
+    assert rel(o1, Ar.float() @ Br.float().t() + bias) < 4e-3
 
 
 @pytest.mark.parametrize("M,N1,N2", [(100, 128, 64), (3000, 64, 768), (50432 // 8, 768, 64)])

@@ -1,5 +1,8 @@
-"""GEMM microbenchmark on the ViT-B/16 step's shapes (dev tool): every lc_gemm_nt tile variant,
-random bf16 operands, HIP-event timing on the launch stream, interleaved rounds."""
+"""GEMM microbenchmark on the ViT-B/16 step's shapes (dev tool): lc_gemm_nt tile variants,
+random bf16 operands, HIP-event timing on the launch stream, interleaved rounds.
+
+  VARIANTS=1,5,5n  (5n = ping-pong without the split-K workspace)   SQUARE=1 adds 4096^3/8192^3
+"""
 import os
 import sys
 
@@ -8,60 +11,77 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "lifelong-clip_amd")]
 import torch  # noqa: E402
 
 from lcclip import _lib, ops  # noqa: E402
+from lcclip._lib import call, ptr, stream_of  # noqa: E402
 
 M = int(os.environ.get("M", 50432))
-SHAPES = [  # (name, N, K, epi)
-    ("qkv_fwd", 2304, 768, ops.EPI_BF16), ("out_fwd", 768, 768, ops.EPI_BF16),
-    ("fc1_fwd", 3072, 768, ops.EPI_GELU_D), ("fc2_fwd", 768, 3072, ops.EPI_BF16),
-    ("fc2_dx", 3072, 768, ops.EPI_MUL), ("fc1_dx", 768, 3072, ops.EPI_BF16),
-    ("out_dx", 768, 768, ops.EPI_BF16), ("qkv_dx", 768, 2304, ops.EPI_BF16),
+SHAPES = [  # (name, M, N, K, epi)
+    ("qkv_fwd", M, 2304, 768, ops.EPI_BF16), ("out_fwd", M, 768, 768, ops.EPI_BF16),
+    ("fc1_fwd", M, 3072, 768, ops.EPI_GELU_D), ("fc2_fwd", M, 768, 3072, ops.EPI_BF16),
+    ("fc2_dx", M, 3072, 768, ops.EPI_MUL), ("fc1_dx", M, 768, 3072, ops.EPI_BF16),
+    ("out_dx", M, 768, 768, ops.EPI_BF16), ("qkv_dx", M, 768, 2304, ops.EPI_BF16),
 ]
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "1,2,3").split(",")]
+if os.environ.get("SQUARE"):
+    SHAPES += [("sq4096", 4096, 4096, 4096, ops.EPI_BF16), ("sq8192", 8192, 8192, 8192, ops.EPI_BF16)]
+VARIANTS = os.environ.get("VARIANTS", "1,2,3").split(",")
 dev = torch.device("cuda:0")
 lib = _lib.load()
 torch.manual_seed(0)
-Kmax, Nmax = 3072, 3072
-A = torch.randn(M, Kmax, device=dev).to(torch.bfloat16)
+Mmax = max(s[1] for s in SHAPES)
+Kmax = max(s[3] for s in SHAPES)
+Nmax = max(s[2] for s in SHAPES)
+A = torch.randn(Mmax, Kmax, device=dev).to(torch.bfloat16)
 Bw = (torch.randn(Nmax, Kmax, device=dev) * 0.03).to(torch.bfloat16)
 bias = torch.randn(Nmax, device=dev)
-o0 = torch.empty(M, Nmax, device=dev, dtype=torch.bfloat16)
-o1 = torch.empty(M, Nmax, device=dev, dtype=torch.bfloat16)
-aux = torch.randn(M, Nmax, device=dev).to(torch.bfloat16)
+o0 = torch.empty(Mmax * Nmax, device=dev, dtype=torch.bfloat16)
+o1 = torch.empty(Mmax * Nmax, device=dev, dtype=torch.bfloat16)
+aux = torch.randn(Mmax * Nmax, device=dev).to(torch.bfloat16)
+
+
+def launch(v, m, N, K, epi, a, b, out0, kw):
+    if v.endswith("n"):  # no split-K workspace
+        out1, ax, bs = kw.get("out1"), kw.get("aux"), kw.get("bias")
+        call("lc_gemm_nt", stream_of(a), epi, m, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+             ptr(bs), 1.0, ptr(out0), N, ptr(out1), N if out1 is not None else 0, ptr(ax),
+             N if ax is not None else 0)
+    else:
+        ops.gemm_nt(a, b, epi, out0, **kw)
+
+
 res = {}
 reps = int(os.environ.get("REPS", 10))
 for rnd in range(3):
-    for name, N, K, epi in SHAPES:
+    for name, m, N, K, epi in SHAPES:
         for v in VARIANTS:
-            if v in (3, 5, 6) and N % 256:
+            t = int(v.rstrip("n"))
+            if t in (3, 5, 6) and N % 256:
                 continue
-            lib.lc_gemm_set_tile(v)
-            a = A[:, :K]
+            lib.lc_gemm_set_tile(t)
+            a = A[:m, :K]
             b = Bw[:N, :K]
-            kw = {}
+            out0 = o0[:m * N].view(m, N)
             if epi in (ops.EPI_GELU, ops.EPI_GELU_D):
-                kw = dict(bias=bias[:N], out1=o1[:, :N])
+                kw = dict(bias=bias[:N], out1=o1[:m * N].view(m, N))
             elif epi in (ops.EPI_GELU_BWD, ops.EPI_MUL):
-                kw = dict(aux=aux[:, :N])
+                kw = dict(aux=aux[:m * N].view(m, N))
             else:
                 kw = dict(bias=bias[:N])
-            ops.gemm_nt(a, b, epi, o0[:, :N], **kw)
+            launch(v, m, N, K, epi, a, b, out0, kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                ops.gemm_nt(a, b, epi, o0[:, :N], **kw)
+                launch(v, m, N, K, epi, a, b, out0, kw)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / reps
             res.setdefault((name, v), []).append(ms)
 lib.lc_gemm_set_tile(0)
-tot = {v: 0.0 for v in VARIANTS}
-for name, N, K, epi in SHAPES:
-    line = f"{name:8s} N={N:5d} K={K:5d}"
+for name, m, N, K, epi in SHAPES:
+    line = f"{name:8s} M={m:6d} N={N:5d} K={K:5d}"
     for v in VARIANTS:
         if (name, v) not in res:
             line += f" | v{v}:   -   "
             continue
         ms = min(res[(name, v)])
-        tf = 2 * M * N * K / ms / 1e9
+        tf = 2 * m * N * K / ms / 1e9
         line += f" | v{v}: {ms * 1e3:7.1f}us {tf:6.0f}TF"
     print(line, flush=True)
