@@ -118,6 +118,31 @@ def pmc_traffic():
     return fam["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
+def time_train_transform(B, dev, reps=20):
+    """The GPU train transform (lcclip.transforms) on a CIFAR-shaped batch,
+    fused into conv1's patch layout: average launch time with HIP events on its stream, and the
+    HBM rate of its algorithmic bytes (input f32 32x32 images + bf16 patch rows written).
+    Reported beside the step; not part of `value`."""
+    from lcclip.transforms import TrainTransform
+    x = torch.randint(0, 256, (B, 3, 32, 32), device=dev).float() / 255
+    tf = TrainTransform.for_dataset("cifar100", generator=torch.Generator().manual_seed(0))
+    prm = tf.draw()
+    out = tf(x, params=prm, layout="patches")
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        tf(x, params=prm, layout="patches")
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    nbytes = x.numel() * 4 + out.numel() * 2
+    return {"kernel": "train_transform_kernel (quantise + resize 32->224 + pad-crop + flip + "
+                      "normalise, written as conv1 bf16 patch rows)",
+            "batch": B, "avg_launch_us": round(us, 2), "algorithmic_bytes": nbytes,
+            "achieved_GBps": round(nbytes / (us * 1e-6) / 1e9, 1), "peak_GBps": PEAK_HBM / 1e9}
+
+
 def cpu_baseline(seconds_cap=30.0):
     """The oracle (fp32 PyTorch-CPU restatement) at BASELINE config 1: LoRA both towers, B = 16,
     C = 16, one full step (fwd, CE-on-probs, bwd, AdamW)."""
@@ -207,6 +232,7 @@ def main():
     with GemmTimer(ops) as gt:
         trainer.eager_step(x, y, tok)
     gs = gt.summary()
+    tf_stats = time_train_transform(B, dev)
 
     if rank == 0:
         f_img = F_IMG[args.method]
@@ -248,6 +274,7 @@ def main():
                          "launches_per_step": gs["pp_n"],
                          "avg_launch_ms": round(gs["pp_ms"] / n_pp, 4),
                          "all_gemm_share_of_step": round(gs["ms"] / ms, 3)},
+            "train_transform": tf_stats,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()

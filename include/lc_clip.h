@@ -124,6 +124,20 @@ int lc_attn_bwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, lo
                 const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
                 int causal);
 
+/* GPU train transform of the online step: the torchvision Compose of methods/_trainer.py:212-242
+ * as applied to the batch at methods/adapter_clip.py:81 — optional uint8 round trip of the
+ * autoaug branch (quantize: (x*255).type(uint8).float()/255, _trainer.py:216/229; the
+ * AutoAugment op itself is not applied), Resize((R,R)) bilinear align_corners=False,
+ * RandomCrop(R, padding=pad) at offset (crop_i, crop_j) of the zero-padded image,
+ * RandomHorizontalFlip when flip != 0 (torchvision draws one decision per batch call),
+ * Normalize(mean, std). x: f32 NCHW [n, C, Hin, Win] (ToTensor values in [0,1]); C <= 4;
+ * mean_host / std_host: HOST arrays of C floats. layout 0: out f32 NCHW [n, C, R, R];
+ * layout 1: out bf16 patch rows [n*(R/patch)^2, C*patch*patch] in conv1's (c, ky, kx) order
+ * (the lc_patchify layout, i.e. the transform fused into conv1's im2col). */
+int lc_train_transform(hipStream_t stream, int n, int C, int Hin, int Win, const float* x, int R,
+                       int pad, int crop_i, int crop_j, int flip, const float* mean_host,
+                       const float* std_host, int quantize, int layout, int patch, void* out);
+
 /* f32 -> bf16 cast of n elements (weight staging). */
 int lc_cast_bf16(hipStream_t stream, long n, const float* src, void* dst);
 

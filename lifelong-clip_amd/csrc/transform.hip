@@ -1,0 +1,237 @@
+// GPU train transform of the online step: the torchvision Compose of
+// methods/_trainer.py:236-242 applied to the uint8-quantised batch on the GPU
+// (methods/adapter_clip.py:81):
+//   [autoaug branch, _trainer.py:216/229: x -> (x*255).type(uint8) -> .float()/255]
+//   Resize((R, R))              bilinear, align_corners = False (upsampling: antialias inert)
+//   RandomCrop(R, padding=pad)  zero pad on every side, crop at (crop_i, crop_j)
+//   RandomHorizontalFlip()      whole batch when flip != 0 (torchvision draws once per call)
+//   Normalize(mean, std)        (v - mean[c]) / std[c]  (LDS kernel: v * (1/std) - mean/std)
+// One pass, no intermediate image: every output pixel gathers its 4 bilinear taps straight from
+// the small input (a 32x32 CIFAR image is 12 KB, L2-resident), so the kernel is bound by its
+// output stream. layout 0 writes the f32 NCHW batch the reference feeds the model; layout 1
+// writes the bf16 patch rows of conv1's GEMM ([n*g*g, C*P*P], the lc_patchify layout) directly,
+// skipping the f32 image round trip.
+#include "lc_common.h"
+
+namespace {
+
+struct TfParams {
+  float mean[4], std_[4];
+  float inv_std[4], nbias[4];  // 1/std and -mean/std (the LDS kernel's fused normalise)
+};
+
+// torch upsample_bilinear2d (align_corners = False) source index and weight along one axis
+LC_DEV void lin_src(int dst, float scale, int in, int& i0, int& i1, float& l1) {
+  float src = scale * (dst + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  int i = (int)src;  // floor (src >= 0)
+  i = i < in - 1 ? i : in - 1;
+  float l = src - (float)i;
+  l = l < 0.f ? 0.f : (l > 1.f ? 1.f : l);
+  i0 = i;
+  i1 = i + (i < in - 1 ? 1 : 0);
+  l1 = l;
+}
+
+LC_DEV float quant(float v, int q) {
+  if (!q) return v;
+  const float t = v * 255.0f;                       // (x * 255).type(torch.uint8): truncation
+  int u = (int)t;
+  u = u < 0 ? 0 : (u > 255 ? 255 : u);
+  return (float)u / 255.0f;                        // .type(torch.float32) / 255
+}
+
+__global__ void __launch_bounds__(256)
+train_transform_kernel(int n, int C, int Hin, int Win, const float* __restrict__ x, int R, int pad,
+                       int crop_i, int crop_j, int flip, TfParams tp, int quantize, int layout,
+                       int P, void* __restrict__ out) {
+  const int q4 = R / 4;
+  const long total = (long)n * C * R * q4;
+  const float sh = (float)Hin / (float)R, sw = (float)Win / (float)R;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int xq = (int)(e % q4);
+    const long r1 = e / q4;
+    const int y = (int)(r1 % R);
+    const long r2 = r1 / R;
+    const int c = (int)(r2 % C);
+    const int img = (int)(r2 / C);
+    const float* src = x + ((long)img * C + c) * Hin * Win;
+    float v[4];
+    const int py = y + crop_i - pad;  // row in the resized image (RandomCrop after zero pad)
+    int y0 = 0, y1 = 0;
+    float ly = 0.f;
+    const bool row_in = py >= 0 && py < R;
+    if (row_in) lin_src(py, sh, Hin, y0, y1, ly);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int xo = xq * 4 + k;
+      const int xs = flip ? (R - 1 - xo) : xo;  // hflip after the crop
+      const int px = xs + crop_j - pad;
+      float val = 0.f;                           // RandomCrop's zero fill
+      if (row_in && px >= 0 && px < R) {
+        int x0, x1;
+        float lx;
+        lin_src(px, sw, Win, x0, x1, lx);
+        const float a = quant(src[y0 * Win + x0], quantize), b = quant(src[y0 * Win + x1], quantize);
+        const float cc = quant(src[y1 * Win + x0], quantize), d = quant(src[y1 * Win + x1], quantize);
+        const float top = a * (1.f - lx) + b * lx;
+        const float bot = cc * (1.f - lx) + d * lx;
+        val = top * (1.f - ly) + bot * ly;
+      }
+      v[k] = (val - tp.mean[c]) / tp.std_[c];
+    }
+    if (layout == 0) {
+      float* o = static_cast<float*>(out) + (((long)img * C + c) * R + y) * R + xq * 4;
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      const int g = R / P;
+      const int pyi = y / P, ky = y % P, pxi = (xq * 4) / P, kx = (xq * 4) % P;
+      const long row = ((long)img * g + pyi) * g + pxi;
+      bf16_t* o = static_cast<bf16_t*>(out) + row * (C * P * P) + (c * P + ky) * P + kx;
+      *reinterpret_cast<uint2*>(o) = uint2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    }
+  }
+}
+
+// Per output row / column of the workgroup's image: the two source taps and the weight of the
+// second after crop, pad and flip (ok = 0: RandomCrop's zero fill). Built once per workgroup in
+// LDS. Each thread owns FIXED output columns (their taps live in registers) and walks rows, so a
+// pixel costs four LDS tap reads and seven FMAs; the row tap is one LDS read per row.
+struct Tap {
+  int i0, i1;
+  float l1;
+  int ok;
+};
+
+// NV pixels of one output row from the LDS-resident (quantised) image; normalise as
+// x * (1/std) - mean/std, within one f32 rounding of torchvision's (x - mean) / std.
+template <int NV>
+LC_DEV void tf_row(const float* __restrict__ simg, const Tap& ry, const Tap (&cx)[NV], int c,
+                   int Hin, int Win, float inv, float bias, float (&v)[NV]) {
+  const float* r0 = simg + (c * Hin + ry.i0) * Win;
+  const float* r1 = simg + (c * Hin + ry.i1) * Win;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float val = 0.f;
+    if (ry.ok & cx[k].ok) {
+      const float top = r0[cx[k].i0] * (1.f - cx[k].l1) + r0[cx[k].i1] * cx[k].l1;
+      const float bot = r1[cx[k].i0] * (1.f - cx[k].l1) + r1[cx[k].i1] * cx[k].l1;
+      val = top * (1.f - ry.l1) + bot * ry.l1;
+    }
+    v[k] = __builtin_fmaf(val, inv, bias);
+  }
+}
+
+// Small inputs (CIFAR: 3 x 32 x 32 f32 = 12 KiB): a workgroup stages the quantised image in LDS
+// once and streams its share of the output in the final order, 16 B per lane per store —
+// coalesced whole rows (layout 0: NCHW f32) or whole patch rows (layout 1: conv1's bf16 im2col,
+// patch 16). Work split: layout 0 — thread = 4 fixed columns, rows strided over the workgroups
+// of the image (gridDim.y); layout 1 — thread = one 8-column chunk of a patch row and a fixed
+// patch column, walking the patch rows.
+template <int LAYOUT>
+__global__ void __launch_bounds__(256)
+train_transform_lds_kernel(int C, int Hin, int Win, const float* __restrict__ x, int R, int pad,
+                           int crop_i, int crop_j, int flip, TfParams tp, int quantize,
+                           void* __restrict__ out) {
+  extern __shared__ float simg[];  // [C*Hin*Win] image, then the row and column tap tables
+  const int img = blockIdx.x;
+  const int tot = C * Hin * Win;
+  Tap* rows = reinterpret_cast<Tap*>(simg + ((tot + 3) & ~3));
+  Tap* cols = rows + R;
+  const float* src = x + (long)img * tot;
+  for (int k = threadIdx.x; k < tot; k += blockDim.x) simg[k] = quant(src[k], quantize);
+  const float sh = (float)Hin / (float)R, sw = (float)Win / (float)R;
+  for (int k = threadIdx.x; k < 2 * R; k += blockDim.x) {
+    const bool is_row = k < R;
+    const int o = is_row ? k : k - R;
+    // row: RandomCrop offset only; column: hflip of the cropped window, then the offset
+    const int p = is_row ? o + crop_i - pad : (flip ? R - 1 - o : o) + crop_j - pad;
+    Tap tp_{0, 0, 0.f, 0};
+    if (p >= 0 && p < R) {
+      lin_src(p, is_row ? sh : sw, is_row ? Hin : Win, tp_.i0, tp_.i1, tp_.l1);
+      tp_.ok = 1;
+    }
+    (is_row ? rows : cols)[o] = tp_;
+  }
+  __syncthreads();
+  if constexpr (LAYOUT == 0) {
+    const int q4 = R / 4, nrg = blockDim.x / q4;
+    const int xq = threadIdx.x % q4, rg = threadIdx.x / q4;
+    if (rg >= nrg) return;
+    Tap cx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cx[k] = cols[xq * 4 + k];
+    float* o = static_cast<float*>(out) + (long)img * C * R * R + xq * 4;
+    for (int r = blockIdx.y * nrg + rg; r < C * R; r += gridDim.y * nrg) {
+      const int c = r / R, y = r - c * R;
+      float v[4];
+      tf_row<4>(simg, rows[y], cx, c, Hin, Win, tp.inv_std[c], tp.nbias[c], v);
+      *reinterpret_cast<float4*>(o + (long)r * R) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    constexpr int P = 16;
+    const int g = R / P, row_len = C * P * P, per_row = row_len / 8, npg = blockDim.x / per_row;
+    const int chunk = threadIdx.x % per_row, pg = threadIdx.x / per_row;
+    const int pxi = blockIdx.y * npg + pg;
+    if (pg >= npg || pxi >= g) return;
+    const int col = chunk * 8, c = col / (P * P), rem = col % (P * P);
+    const int ky = rem / P, x0 = pxi * P + rem % P;
+    Tap cx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cx[k] = cols[x0 + k];
+    const float inv = tp.inv_std[c], bias = tp.nbias[c];
+    bf16_t* o = static_cast<bf16_t*>(out) + ((long)img * g * g + pxi) * row_len + col;
+    for (int pyi = 0; pyi < g; ++pyi) {
+      float v[8];
+      tf_row<8>(simg, rows[pyi * P + ky], cx, c, Hin, Win, inv, bias, v);
+      *reinterpret_cast<uint4*>(o + (long)pyi * g * row_len) =
+          uint4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int lc_train_transform(hipStream_t st, int n, int C, int Hin, int Win, const float* x, int R,
+                       int pad, int crop_i, int crop_j, int flip, const float* mean_host,
+                       const float* std_host, int quantize, int layout, int patch, void* out) {
+  LC_CHECK_ARG(n > 0 && C >= 1 && C <= 4 && Hin > 0 && Win > 0 && R > 0 && R % 4 == 0);
+  LC_CHECK_ARG(pad >= 0 && crop_i >= 0 && crop_j >= 0 && crop_i <= 2 * pad && crop_j <= 2 * pad);
+  LC_CHECK_ARG(mean_host != nullptr && std_host != nullptr && x != nullptr && out != nullptr);
+  LC_CHECK_ARG(layout == 0 || (layout == 1 && patch > 0 && patch % 4 == 0 && R % patch == 0));
+  TfParams tp{};
+  for (int c = 0; c < C; ++c) {
+    LC_CHECK_ARG(std_host[c] != 0.f);
+    tp.mean[c] = mean_host[c];
+    tp.std_[c] = std_host[c];
+    tp.inv_std[c] = 1.0f / std_host[c];
+    tp.nbias[c] = -mean_host[c] / std_host[c];
+  }
+  const size_t img_bytes = (size_t)((C * Hin * Win + 3) & ~3) * sizeof(float) + 2 * R * 16;
+  if (img_bytes <= 64 * 1024 && layout == 0 && R / 4 <= 256) {
+    const int q4 = R / 4, nrg = 256 / q4;
+    hipLaunchKernelGGL(train_transform_lds_kernel<0>, dim3(n, 8),  // 8 workgroups per image
+                       dim3(nrg * q4), img_bytes, st, C,
+                       Hin, Win, x, R, pad, crop_i, crop_j, flip, tp, quantize, out);
+    LC_LAUNCH_RET();
+  }
+  if (img_bytes <= 64 * 1024 && layout == 1 && patch == 16 && C * 32 <= 256) {
+    const int per_row = C * 32, npg = 256 / per_row, g = R / 16;
+    hipLaunchKernelGGL(train_transform_lds_kernel<1>, dim3(n, (g + npg - 1) / npg),
+                       dim3(npg * per_row), img_bytes, st, C, Hin, Win, x, R, pad, crop_i, crop_j,
+                       flip, tp, quantize, out);
+    LC_LAUNCH_RET();
+  }
+  // large inputs: per-pixel gathers straight from global memory
+  const long total = (long)n * C * R * (R / 4);
+  long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(train_transform_kernel, dim3((unsigned)blocks), dim3(256), 0, st, n, C, Hin,
+                     Win, x, R, pad, crop_i, crop_j, flip, tp, quantize, layout, patch, out);
+  LC_LAUNCH_RET();
+}
+
+}  // extern "C"

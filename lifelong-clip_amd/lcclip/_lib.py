@@ -33,6 +33,8 @@ SIGNATURES = {
     "lc_eot_rows": [P, c_int, c_int, P, P],
     "lc_attn_fwd": [P, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int],
     "lc_attn_bwd": [P, c_int, c_int, c_int, P, c_long, P, P, c_long, P, P, c_long, c_int],
+    "lc_train_transform": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, P,
+                           P, c_int, c_int, c_int, P],
     "lc_cast_bf16": [P, c_long, P, P],
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],

@@ -368,15 +368,23 @@ class ImageTower:
         v = self.visual
         self._stage()
         dev = img.device
-        n = img.shape[0]
         P = v.patch_size
         g = v.input_resolution // P
         npch = g * g
         L = npch + 1
         D = v.width
-        img = img.contiguous().to(F32)
-        patches = _empty((n * npch, 3 * P * P), BF16, dev)
-        ops.patchify(img, P, patches)
+        if img.dim() == 2:
+            # conv1's bf16 im2col rows, already produced by the fused train transform
+            # (lcclip.transforms.TrainTransform(..., layout="patches"))
+            if img.dtype != BF16 or img.shape[1] != 3 * P * P or img.shape[0] % npch:
+                raise ValueError(f"patch input must be bf16 [n*{npch}, {3 * P * P}]")
+            n = img.shape[0] // npch
+            patches = img.contiguous()
+        else:
+            n = img.shape[0]
+            img = img.contiguous().to(F32)
+            patches = _empty((n * npch, 3 * P * P), BF16, dev)
+            ops.patchify(img, P, patches)
         pe = _empty((n * npch, D), F32, dev)
         ops.gemm_nt(patches, self.conv_w, EPI_F32, pe)
         xa = _empty((n * L, D), F32, dev)

@@ -316,7 +316,9 @@ class CLIP(nn.Module):
         return self._text_tower
 
     def encode_image(self, image):
-        return self.visual(image.type(self.dtype))
+        # model.py:938-939 casts the image batch to the model dtype; a 2-D input is conv1's bf16
+        # patch rows from the fused train transform and is passed through as is
+        return self.visual(image if image.dim() == 2 else image.type(self.dtype))
 
     def encode_text(self, text):
         return lc_autograd.tower_apply(self.text_tower, self.transformer, text, self.training)

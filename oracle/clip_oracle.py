@@ -368,6 +368,34 @@ def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-
     return loss.detach(), probs.detach(), fi.detach(), ft.detach(), grads, new
 
 
+# ----------------------------------------------------------------------------- train transform
+def train_transform(x, inp_size, padding, crop_i, crop_j, flip, mean, std, quantize=True):
+    """methods/_trainer.py:212-242 on a batch tensor (torchvision tensor semantics: one parameter
+    draw per call, shared by the batch): the autoaug branch's uint8 round trip (:216, :229; the
+    AutoAugment op between them is NOT restated), Resize((S, S)) — torchvision's F.resize is
+    F.interpolate(bilinear, align_corners=False) (antialias is inert when upsampling) —,
+    RandomCrop(S, padding) = zero F.pad then the [i:i+S, j:j+S] window, hflip, Normalize
+    ((x - mean) / std)."""
+    if quantize:
+        x = (x * 255).to(torch.uint8).to(torch.float32) / 255
+    x = F.interpolate(x, size=(inp_size, inp_size), mode="bilinear", align_corners=False)
+    x = F.pad(x, (padding, padding, padding, padding), value=0.0)
+    x = x[:, :, crop_i:crop_i + inp_size, crop_j:crop_j + inp_size]
+    if flip:
+        x = x.flip(-1)
+    m = torch.tensor(mean, dtype=x.dtype).view(1, -1, 1, 1)
+    s = torch.tensor(std, dtype=x.dtype).view(1, -1, 1, 1)
+    return (x - m) / s
+
+
+def patchify(img, patch):
+    """conv1's im2col (model.py:756): [n, C, S, S] -> [n*(S/P)^2, C*P*P] in (c, ky, kx) order."""
+    n, C, S, _ = img.shape
+    g = S // patch
+    t = img.reshape(n, C, g, patch, g, patch).permute(0, 2, 4, 1, 3, 5)
+    return t.reshape(n * g * g, C * patch * patch)
+
+
 # ----------------------------------------------------------------------------- synthetic data
 def synthetic_images(n, res=224, seed=0):
     """U[0,1) images normalised with the CIFAR-100 statistics

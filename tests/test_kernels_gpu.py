@@ -256,6 +256,68 @@ def test_attention_fwd_bwd(ops, dev, n, L, H, causal):
     assert rel(g[2], v.grad) < 2e-2
 
 
+# ------------------------------------------------------------------------------- train transform
+@pytest.mark.parametrize("params", [(0, 0, False), (8, 8, True), (3, 5, True), (4, 4, False)])
+def test_train_transform_vs_oracle(dev, params):
+    """lc_train_transform (methods/_trainer.py:212-242 minus the AutoAugment op) vs the oracle's
+    torch restatement on CIFAR-shaped ToTensor batches: f32 NCHW within 2e-6 absolute (the
+    bilinear taps are summed in a different order, normalise as one FMA), the fused bf16 patch layout equal to
+    patchify(oracle) up to one bf16 rounding step."""
+    import oracle.clip_oracle as o
+    from lcclip.transforms import TrainTransform
+    i, j, flip = params
+    g = torch.Generator().manual_seed(sum(params) + 1)
+    x = torch.randint(0, 256, (6, 3, 32, 32), generator=g).float() / 255  # ToTensor values
+    tf = TrainTransform.for_dataset("cifar100")
+    ref = o.train_transform(x, 224, 4, i, j, flip, tf.mean, tf.std, quantize=True)
+    got = tf(x.to(dev), params=params)
+    assert got.shape == (6, 3, 224, 224)
+    assert (got.cpu() - ref).abs().max().item() < 2e-6
+    pt = tf(x.to(dev), params=params, layout="patches")
+    pref = o.patchify(ref, 16)
+    assert pt.shape == (6 * 196, 768) and pt.dtype == BF
+    d = (pt.float().cpu() - pref).abs()
+    assert (d <= pref.abs() * 2 ** -7 + 1e-6).all()
+    # a same-size resize with identity normalisation isolates the uint8 round trip (and the
+    # flip): the kernel equals torch bit for bit, with and without the quantisation
+    for q in (False, True):
+        tf2 = TrainTransform((0.0,) * 3, (1.0,) * 3, inp_size=32, padding=0, autoaug=q)
+        ref2 = o.train_transform(x, 32, 0, 0, 0, flip, tf2.mean, tf2.std, quantize=q)
+        assert torch.equal(tf2(x.to(dev), params=(0, 0, flip)).cpu(), ref2)
+
+
+def test_train_transform_large_input_path(dev):
+    """Inputs too large for the LDS-staged kernel (3 x 96 x 96 f32 > 64 KiB) take the gather
+    kernel: same oracle bound, both layouts."""
+    import oracle.clip_oracle as o
+    from lcclip.transforms import TrainTransform
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 256, (3, 3, 96, 96), generator=g).float() / 255
+    tf = TrainTransform.for_dataset("imagenet-r")
+    ref = o.train_transform(x, 224, 4, 6, 1, True, tf.mean, tf.std, quantize=True)
+    got = tf(x.to(dev), params=(6, 1, True))
+    assert (got.cpu() - ref).abs().max().item() < 2e-6
+    pt = tf(x.to(dev), params=(6, 1, True), layout="patches")
+    pref = o.patchify(ref, 16)
+    assert ((pt.float().cpu() - pref).abs() <= pref.abs() * 2 ** -7 + 1e-6).all()
+
+
+def test_transform_patches_feed_the_image_tower(dev):
+    """The fused patch layout is a drop-in input of the image tower: same features as the f32
+    image batch through lc_patchify."""
+    from lcclip import AdapterCLIP
+    from lcclip.transforms import TrainTransform
+    torch.manual_seed(0)
+    w = AdapterCLIP("ViT-B/16", peft_method="adapter", peft_encoder="both", device=dev)
+    x = (torch.randint(0, 256, (4, 3, 32, 32), device=dev).float() / 255)
+    tf = TrainTransform.for_dataset("cifar100")
+    prm = tf.draw()
+    with torch.no_grad():
+        f_img = w.encode_image(tf(x, params=prm))
+        f_pt = w.encode_image(tf(x, params=prm, layout="patches"))
+    assert rel(f_pt, f_img) < 1e-6
+
+
 # ------------------------------------------------------------------------------- PEFT
 @pytest.mark.parametrize("D,M,keep", [(768, 1000, 1.0), (128, 77, 1.0), (512, 300, 0.9)])
 def test_adapter_fwd_bwd(ops, dev, D, M, keep):

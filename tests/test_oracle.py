@@ -158,3 +158,49 @@ def test_oracle_reproduces_golden(method):
     # loss band (C = 3)
     hi = math.log(2 + math.e)
     assert hi - 1 <= loss.item() <= hi
+
+
+# ----------------------------------------------------------------- train transform (§8(f) f2)
+def test_train_transform_restatement_identities():
+    """Pins of oracle.train_transform (methods/_trainer.py:212-242) that do not depend on torch's
+    op internals: the align_corners=False bilinear source mapping at a few pixels, RandomCrop's
+    zero padding (normalised to -mean/std), the flip as a mirror, and the uint8 round trip as
+    truncation of the f32 product x*255 (the `.type(torch.uint8)` cast)."""
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 256, (2, 3, 32, 32), generator=g).float() / 255
+    mean, std = (0.5071, 0.4867, 0.4408), (0.2675, 0.2565, 0.2761)
+    out = o.train_transform(x, 224, 4, 0, 0, False, mean, std, quantize=False)
+    # crop offset (0, 0) of the 4-padded image: rows/cols 0..3 are padding
+    for c in range(3):
+        assert torch.allclose(out[:, c, :4, :], torch.full_like(out[:, c, :4, :], -mean[c] / std[c]))
+        assert torch.allclose(out[:, c, :, :4], torch.full_like(out[:, c, :, :4], -mean[c] / std[c]))
+    # interior pixel (y, x) = (4 + 100, 4 + 37) of the resized image: src = (d + 0.5) * 32/224 - 0.5
+    up = (out[:, :, 104, 41] * torch.tensor(std) + torch.tensor(mean))
+    sy, sx = (100 + 0.5) * 32 / 224 - 0.5, (37 + 0.5) * 32 / 224 - 0.5
+    y0, x0 = int(math.floor(sy)), int(math.floor(sx))
+    ly, lx = sy - y0, sx - x0
+    want = ((1 - ly) * ((1 - lx) * x[:, :, y0, x0] + lx * x[:, :, y0, x0 + 1])
+            + ly * ((1 - lx) * x[:, :, y0 + 1, x0] + lx * x[:, :, y0 + 1, x0 + 1]))
+    assert torch.allclose(up, want, atol=1e-6)
+    # the edge clamps to the first source pixel (src < 0 -> 0)
+    e = out[:, :, 4, 4] * torch.tensor(std) + torch.tensor(mean)
+    assert torch.allclose(e, x[:, :, 0, 0], atol=1e-6)
+    # flip mirrors the cropped window
+    fl = o.train_transform(x, 224, 4, 3, 5, True, mean, std, quantize=False)
+    nf = o.train_transform(x, 224, 4, 3, 5, False, mean, std, quantize=False)
+    assert torch.equal(fl, nf.flip(-1))
+    # uint8 round trip = trunc(f32(x) * 255) / 255
+    q = o.train_transform(x, 32, 0, 0, 0, False, (0.0,) * 3, (1.0,) * 3, quantize=True)
+    xn = x.numpy().astype(np.float32)
+    want_q = np.trunc(xn * np.float32(255)).astype(np.float32) / np.float32(255)
+    assert np.array_equal(q.numpy(), want_q)
+
+
+def test_patchify_matches_conv1():
+    """oracle.patchify's (c, ky, kx) column order is conv1's weight layout (model.py:709-713)."""
+    torch.manual_seed(0)
+    img = torch.randn(2, 3, 32, 32)
+    w = torch.randn(8, 3, 16, 16)
+    conv = torch.nn.functional.conv2d(img, w, stride=16)  # [2, 8, 2, 2]
+    gemm = o.patchify(img, 16) @ w.reshape(8, -1).t()     # [2*4, 8]
+    assert torch.allclose(gemm, conv.permute(0, 2, 3, 1).reshape(8, 8), atol=1e-4)
