@@ -170,6 +170,15 @@ int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
                    void* dz, long ldz);
 
+/* Adapter weight and bias gradients of one application, accumulated (f32, one launch):
+ *   dWu [D,64] += scale * gout^T h      dbu [D]  += scale * sum_m gout[m]   (up_proj)
+ *   dWd [64,D] += dpre^T z              dbd [64] += sum_m dpre[m]           (down_proj)
+ * gout, z bf16 [M,D] (row strides ldg, ldz); h, dpre bf16 [M,64] contiguous. dbu / dbd may be
+ * NULL. Replaces: the autograd weight/bias reductions of adapter.py:38-40 applied at :59-62. */
+int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                     const void* z, long ldz, const void* dpre, float scale, float* dWu,
+                     float* dbu, float* dWd, float* dbd);
+
 /* *flag |= any(!isfinite(g))  (GradScaler's inf check, _trainer.py:163, adapter_clip.py:94). */
 int lc_check_finite(hipStream_t stream, long n, const float* g, int* flag);
 

@@ -662,6 +662,209 @@ gemm_tn_kernel(int M, int N1, int N2, int chunk_rows, const bf16_t* __restrict__
       }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide x skinny TN reduction (the PEFT weight gradients): P[n][j] = sum_m W[m][n] S[m][j] for a
+// wide operand W [M, Nw] (activations / output gradients, Nw = 768 / 2304) and a skinny one
+// S [M, 64] (adapter bottleneck, zero-padded LoRA rank), stored as C[n][j] or, transposed, C[j][n].
+// These are HBM streams (≈128 FLOP per byte of W at most), so the design is about bytes in flight:
+// one 512-thread workgroup per CU owns a 128-column W panel and a long contiguous chunk of rows,
+// streamed through a 5-slot global_load_lds ring (64 rows x (256 + 128) B = 24 KiB per slot, four
+// slots in flight), and adds its 128 x 64 partial once with f32 atomics at the end (one partial
+// per workgroup instead of one per 64x64 tile and short chunk). Column sums (bias gradients) ride
+// on the MFMA as products with a ones fragment. Up to two problems per launch (adapter: dWu and
+// dWd in one grid).
+struct TnProb {
+  const bf16_t* W;
+  long ldw;
+  const bf16_t* S;
+  long lds;
+  float* C;
+  long ldc;
+  int Nw, ns, trans;  // P is Nw x ns; trans: C[j][n] instead of C[n][j]
+  float alpha;
+  float* cs_w;        // += cs_w_scale * sum_m W[m][n]   (n < Nw), or nullptr
+  float cs_w_scale;
+  float* cs_s;        // += cs_s_scale * sum_m S[m][j]   (j < ns), or nullptr
+  float cs_s_scale;
+  int M, n_chunks, n_tiles, wgs;  // row-block walkers per panel, W panels, workgroups
+};
+
+constexpr int TNW_STAGES = 5;
+constexpr int TNW_SLOT = 64 * 256 + 64 * 128;  // W panel 64 x 128 bf16 + S 64 x 64 bf16
+constexpr int TNW_LOADS = (16 + 8) / 8;        // glds instructions per wave per slot
+
+// LDS images are XOR-swizzled in 32-B units so that the 8 rows {0..3, 8..11} (+16) one
+// ds_read_b64_tr_b16 pass of 32 lanes touches land in 8 distinct 32-B bank groups.
+//   W rows (256 B = 8 units): unit u of row r at u ^ ((r & 3) | ((r >> 1) & 4))
+//   S rows (128 B = 4 units; two rows per 256-B bank span): unit u at u ^ (((r >> 1) & 1) | ((r >> 2) & 2))
+LC_DEV int swz_w(int r) { return (r & 3) | ((r >> 1) & 4); }
+LC_DEV int swz_s(int r) { return ((r >> 1) & 1) | ((r >> 2) & 2); }
+
+// 8 consecutive k-rows (row, row + 4 of the lane's 4-row group) of one 16-column block, as an
+// MFMA operand: lane (g, t) gets column col0 + t, k = 8g .. 8g+7 of the 32-row k-slice.
+template <int ROWB>
+LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
+  auto addr = [&](int r) {
+    const int byte = col * 2;  // within the row
+    const int u = (byte >> 5) ^ (ROWB == 256 ? swz_w(r) : swz_s(r));
+    return lds + r * ROWB + u * 32 + (byte & 31);
+  };
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) bf16x4*)addr(row));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) bf16x4*)addr(row + 4));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// 8 waves: wave w owns W columns 32 (w & 3) .. +31 and S columns 32 (w >> 2) .. +31 of the panel.
+__global__ void __launch_bounds__(512, 1)
+gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
+  __shared__ __attribute__((aligned(16))) char smem[TNW_STAGES * TNW_SLOT];
+  const bool second = (int)blockIdx.x >= p0.wgs;
+  const TnProb& p = second ? p1 : p0;
+  const int bid = second ? blockIdx.x - p0.wgs : blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wsv = wave >> 2;
+  const int g = lane >> 4, t = lane & 15;
+  const int tile = bid % p.n_tiles, cidx = bid / p.n_tiles;
+  // block-cyclic rows: walker cidx takes 64-row blocks cidx, cidx + n_chunks, ... so that the
+  // workgroups of the grid sweep one contiguous band of rows together (DRAM-page locality)
+  const int nblk = (p.M + 63) / 64;
+  if (cidx >= nblk) return;
+  const int nsteps = (nblk - 1 - cidx) / p.n_chunks + 1;
+  auto blk_row = [&](int s) { return (cidx + s * p.n_chunks) * 64; };
+  const int nw_pad = (p.Nw + 63) & ~63;
+  const bool do_csw = p.cs_w != nullptr && wsv == 0;
+  const bool do_css = p.cs_s != nullptr && tile == 0 && wn == 0;
+
+  // DMA of step s into slot s % STAGES. A wave-instruction fills 1 KiB of LDS linearly; the
+  // lane -> (row, unit) map inverts the swizzle (source chosen so that lane*16 is its slot).
+  //   W: 4 rows per piece, lane -> row lane >> 4, position 16-B chunk lane & 15
+  //   S: 8 rows per piece, lane -> row lane >> 3, position chunk lane & 7
+  auto dma = [&](int s) {
+    char* sl = smem + (s % TNW_STAGES) * TNW_SLOT;
+    const int r0 = blk_row(s);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wave * 2 + i;  // 16 W pieces
+      const int lr = piece * 4 + (lane >> 4);
+      const int pc = lane & 15;
+      const int c = (((pc >> 1) ^ swz_w(lr)) << 1) | (pc & 1);  // source 16-B chunk
+      const int r = min(r0 + lr, p.M - 1);
+      int col = tile * 128 + c * 8;
+      col = col < nw_pad ? col : col - 64;  // past a 64-multiple Nw: re-read, masked at the store
+      glds16(p.W + (long)r * p.ldw + col, sl + piece * 1024);
+    }
+    {
+      const int piece = wave;  // 8 S pieces
+      const int lr = piece * 8 + (lane >> 3);
+      const int pc = lane & 7;
+      const int c = (((pc >> 1) ^ swz_s(lr)) << 1) | (pc & 1);
+      const int r = min(r0 + lr, p.M - 1);
+      glds16(p.S + (long)r * p.lds + c * 8, sl + 64 * 256 + piece * 1024);
+    }
+  };
+
+  f32x4 acc[2][2], csw[2], css[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    csw[i] = css[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const short one = (short)0x3F80;
+
+#pragma unroll
+  for (int s = 0; s < TNW_STAGES - 1; ++s)
+    if (s < nsteps) dma(s);
+  for (int s = 0; s < nsteps; ++s) {
+    // own DMA of step s landed (up to STAGES-2 later steps may stay in flight); after the
+    // barrier every wave's has, and every wave is done reading slot (s-1) % STAGES, which the
+    // DMA of step s + STAGES - 1 overwrites
+    const int ahead = min(nsteps - 1 - s, TNW_STAGES - 2);
+    if (ahead >= 3) wait_vmcnt<3 * TNW_LOADS>();
+    else if (ahead == 2) wait_vmcnt<2 * TNW_LOADS>();
+    else if (ahead == 1) wait_vmcnt<TNW_LOADS>();
+    else wait_vmcnt<0>();
+    __syncthreads();
+    if (s + TNW_STAGES - 1 < nsteps) dma(s + TNW_STAGES - 1);
+    const char* sw = smem + (s % TNW_STAGES) * TNW_SLOT;
+    const char* ss = sw + 64 * 256;
+    const int valid = p.M - blk_row(s);  // rows of this block inside M (>= 64: all)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int row = ks * 32 + g * 8 + (t >> 2);
+      const int kb = ks * 32 + g * 8;
+      bf16x8 fw[2], fs[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fw[i] = tr_frag<256>(sw, row, wn * 32 + i * 16 + (t & 3) * 4);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fs[j] = tr_frag<128>(ss, row, wsv * 32 + j * 16 + (t & 3) * 4);
+      bf16x8 ones;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ones[e] = (kb + e < valid) ? one : (short)0;
+      if (valid < 64) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) fs[j][e] = (kb + e < valid) ? fs[j][e] : (short)0;
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fw[i], fs[j], acc[i][j]);
+        if (do_csw) csw[i] = mfma16(fw[i], ones, csw[i]);
+      }
+      if (do_css) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) css[j] = mfma16(ones, fs[j], css[j]);
+      }
+    }
+  }
+  // lane holds P[n = tile*128 + 32wn + 16i + 4g + r][j = 32wsv + 16jj + t]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = tile * 128 + wn * 32 + i * 16 + g * 4 + r;
+      if (n >= p.Nw) continue;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = wsv * 32 + jj * 16 + t;
+        if (j < p.ns) {
+          float* dst = p.trans ? p.C + (long)j * p.ldc + n : p.C + (long)n * p.ldc + j;
+          atomicAdd(dst, acc[i][jj][r] * p.alpha);
+        }
+      }
+      if (do_csw && t == 0) atomicAdd(p.cs_w + n, csw[i][r] * p.cs_w_scale);
+    }
+  if (do_css && g == 0) {
+    // css[jj]: lane holds sum_k S[k][32wsv + 16jj + t] in every r
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = wsv * 32 + jj * 16 + t;
+      if (j < p.ns) atomicAdd(p.cs_s + j, css[jj][0] * p.cs_s_scale);
+    }
+  }
+}
+
+int cu_count();
+
+// Walkers per panel so that the problems of one launch fill about one workgroup per CU.
+void plan_tn(TnProb& p, int total_panels) {
+  // measured (adapter dW, M = 50 432): one walker per CU 60 us; 2 per CU 80 us (twice the
+  // partials to add atomically); contiguous per-walker chunks instead of block-cyclic 80-88 us
+  const int cus = cu_count();
+  const int nblk = (p.M + 63) / 64;
+  int chunks = cus / total_panels;
+  chunks = chunks < 1 ? 1 : chunks;
+  // at least 4 blocks per walker (ring fill)
+  chunks = chunks > nblk / 4 ? (nblk / 4 > 0 ? nblk / 4 : 1) : chunks;
+  p.n_chunks = chunks;
+  p.wgs = p.n_tiles * chunks;
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES>
 int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
@@ -865,6 +1068,31 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
   // of 64 (zero padding); outputs beyond N1 x N2 are masked
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= (N1 + 63) / 64 * 64 &&
                ldb >= (N2 + 63) / 64 * 64 && ldc >= N2);
+  if (N1 <= 64 || N2 <= 64) {
+    // wide x skinny: the skinny side is the 64-column operand; C transposed when it is A
+    const bool a_wide = N2 <= 64;
+    TnProb p{};
+    p.W = static_cast<const bf16_t*>(a_wide ? A : B);
+    p.ldw = a_wide ? lda : ldb;
+    p.S = static_cast<const bf16_t*>(a_wide ? B : A);
+    p.lds = a_wide ? ldb : lda;
+    p.C = C;
+    p.ldc = ldc;
+    p.Nw = a_wide ? N1 : N2;
+    p.ns = a_wide ? N2 : N1;
+    p.trans = a_wide ? 0 : 1;
+    p.alpha = alpha;
+    p.cs_w = a_wide ? colsum : nullptr;
+    p.cs_w_scale = colsum_scale;
+    p.cs_s = a_wide ? nullptr : colsum;
+    p.cs_s_scale = colsum_scale;
+    p.M = M;
+    p.n_tiles = (p.Nw + 127) / 128;
+    plan_tn(p, p.n_tiles);
+    TnProb none{};
+    hipLaunchKernelGGL(gemm_tn_wide_kernel, dim3(p.wgs), dim3(512), 0, stream, p, none);
+    LC_LAUNCH_RET();
+  }
   const int tiles = ((N1 + 63) / 64) * ((N2 + 63) / 64);
   // Enough M-chunks to give ~4 workgroups per CU, each chunk a multiple of 64 rows.
   int splits = (1024 + tiles - 1) / tiles;
@@ -876,6 +1104,49 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
   hipLaunchKernelGGL(gemm_tn_kernel, grid, block, 0, stream, M, N1, N2, chunk,
                      static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(B), ldb, alpha,
                      C, ldc, colsum, colsum_scale);
+  LC_LAUNCH_RET();
+}
+
+int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                     const void* z, long ldz, const void* dpre, float scale, float* dWu,
+                     float* dbu, float* dWd, float* dbd) {
+  LC_CHECK_ARG(M > 0 && D > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0 && ldg >= D &&
+               ldz >= D);
+  LC_CHECK_ARG(dWu != nullptr && dWd != nullptr);
+  TnProb up{}, down{};
+  // dWu[D][64] += scale * gout^T h ; dbu += scale * colsum(gout)
+  up.W = static_cast<const bf16_t*>(gout);
+  up.ldw = ldg;
+  up.S = static_cast<const bf16_t*>(h);
+  up.lds = 64;
+  up.C = dWu;
+  up.ldc = 64;
+  up.Nw = D;
+  up.ns = 64;
+  up.trans = 0;
+  up.alpha = scale;
+  up.cs_w = dbu;
+  up.cs_w_scale = scale;
+  up.M = M;
+  up.n_tiles = (D + 127) / 128;
+  // dWd[64][D] += dpre^T z = (z^T dpre)^T ; dbd += colsum(dpre)
+  down.W = static_cast<const bf16_t*>(z);
+  down.ldw = ldz;
+  down.S = static_cast<const bf16_t*>(dpre);
+  down.lds = 64;
+  down.C = dWd;
+  down.ldc = D;
+  down.Nw = D;
+  down.ns = 64;
+  down.trans = 1;
+  down.alpha = 1.0f;
+  down.cs_s = dbd;
+  down.cs_s_scale = 1.0f;
+  down.M = M;
+  down.n_tiles = (D + 127) / 128;
+  plan_tn(up, 2 * up.n_tiles);
+  plan_tn(down, 2 * down.n_tiles);
+  hipLaunchKernelGGL(gemm_tn_wide_kernel, dim3(up.wgs + down.wgs), dim3(512), 0, stream, up, down);
   LC_LAUNCH_RET();
 }
 

@@ -317,10 +317,10 @@ class BlockStack:
         with self._side():
             if getattr(self, "_gs", None) is not None:
                 dpre.record_stream(self._gs)
-            ops.gemm_tn(gout, h, self._grad(grads, ad.up_proj.weight), alpha=ad.scale,
-                        colsum=self._grad(grads, ad.up_proj.bias), colsum_scale=ad.scale)
-            ops.gemm_tn(dpre, z, self._grad(grads, ad.down_proj.weight), alpha=1.0,
-                        colsum=self._grad(grads, ad.down_proj.bias), colsum_scale=1.0)
+            ops.adapter_wgrad(gout, h, z, dpre, ad.scale, self._grad(grads, ad.up_proj.weight),
+                              self._grad(grads, ad.up_proj.bias),
+                              self._grad(grads, ad.down_proj.weight),
+                              self._grad(grads, ad.down_proj.bias))
         return dz
 
     def _lora_grad(self, dY, X, A, B, scaling, grads, padded):

@@ -177,6 +177,23 @@ def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
          ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz), dz.stride(0))
 
 
+def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
+    """dWu += scale gout^T h, dbu += scale colsum(gout), dWd += dpre^T z, dbd += colsum(dpre)."""
+    M, D = gout.shape
+    for t, name in ((gout, "gout"), (z, "z")):
+        _rowmajor(t, BF16, name)
+    for t, name in ((h, "h"), (dpre, "dpre")):
+        if t.dtype != BF16 or not t.is_contiguous() or t.shape != (M, 64):
+            raise ValueError(f"{name} must be contiguous bf16 [M, 64]")
+    if z.shape != (M, D) or dWu.shape != (D, 64) or dWd.shape != (64, D):
+        raise ValueError("adapter_wgrad shape mismatch")
+    for t in (dWu, dWd, dbu, dbd):
+        if t is not None and (t.dtype != F32 or not t.is_contiguous()):
+            raise ValueError("gradient buffers must be contiguous f32")
+    call("lc_adapter_wgrad", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
+         z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd))
+
+
 def check_finite(g, flag):
     call("lc_check_finite", stream_of(g), g.numel(), ptr(g), ptr(flag))
 

@@ -158,6 +158,25 @@ def test_gemm_tn(ops, dev, M, N1, N2):
     assert rel(cs - 1, 0.25 * A.float().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("M,D", [(77 * 10, 512), (50432 // 8 + 37, 768)])
+def test_adapter_wgrad(ops, dev, M, D):
+    """Both adapter weight/bias gradients in one launch (ragged M: masked last step)."""
+    torch.manual_seed(5)
+    gout = torch.randn(M, D, device=dev).to(BF)
+    z = torch.randn(M, D, device=dev).to(BF)
+    h = torch.randn(M, 64, device=dev).to(BF)
+    dpre = torch.randn(M, 64, device=dev).to(BF)
+    dWu = torch.full((D, 64), 2.0, device=dev)
+    dbu = torch.full((D,), 2.0, device=dev)
+    dWd = torch.full((64, D), 2.0, device=dev)
+    dbd = torch.full((64,), 2.0, device=dev)
+    ops.adapter_wgrad(gout, h, z, dpre, 0.1, dWu, dbu, dWd, dbd)
+    assert rel(dWu - 2, 0.1 * gout.float().t() @ h.float()) < 1e-5
+    assert rel(dbu - 2, 0.1 * gout.float().sum(0)) < 1e-5
+    assert rel(dWd - 2, dpre.float().t() @ z.float()) < 1e-5
+    assert rel(dbd - 2, dpre.float().sum(0)) < 1e-5
+
+
 def test_gemm_tn_masked_rank4(ops, dev):
     """N1 or N2 below 64 (zero-padded [M,64] operands, outputs masked): the LoRA dA / dB path."""
     torch.manual_seed(11)

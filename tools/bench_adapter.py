@@ -23,6 +23,8 @@ dpre = torch.empty(M, 64, device=dev, dtype=bf)
 dz = torch.empty(M, D, device=dev, dtype=bf)
 WuT, WdT = Wu.t().contiguous(), Wd.t().contiguous()
 w = torch.randn(D, device=dev)
+dWu, dbu = torch.zeros(D, 64, device=dev), torch.zeros(D, device=dev)
+dWd, dbd = torch.zeros(64, D, device=dev), torch.zeros(64, device=dev)
 y = torch.empty(M, D, device=dev, dtype=bf)
 mean = torch.empty(M, device=dev)
 rstd = torch.empty(M, device=dev)
@@ -45,6 +47,10 @@ cases = {
     "adapter_fwd keep=.9": (lambda: ops.adapter_fwd(z, Wd, bd, Wu, bu, 0.1, 0.9, 7, resid, x, h),
                             M * D * (2 + 4 + 4) + M * 128),
     "adapter_bwd": (lambda: ops.adapter_bwd(z, h, WuT, WdT, 0.1, 1.0, dpre, dz), M * D * 4 + M * 256),
+    "adapter_wgrad": (lambda: ops.adapter_wgrad(z, h, z, dpre, 0.1, dWu, dbu, dWd, dbd),
+                      M * D * 4 + M * 256),
+    "gemm_tn x2 (old)": (lambda: (ops.gemm_tn(z, h, dWu, alpha=0.1, colsum=dbu, colsum_scale=0.1),
+                                  ops.gemm_tn(dpre, z, dWd, colsum=dbd)), M * D * 4 + M * 256),
     "ln_fwd bf16": (lambda: ops.layernorm_fwd(resid, w, w, y, mean, rstd), M * D * 6),
 }
 for name, (fn, nbytes) in cases.items():
