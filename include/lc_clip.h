@@ -163,7 +163,8 @@ int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, co
                    unsigned long long seed, const unsigned long long* seed_dev,
                    const float* resid, float* xout, long ldx, void* h);
 
-/* Row-local adapter backward: dpre (bf16 [M,64]) and dz = gout + dpre Wd (bf16).
+/* Row-local adapter backward: dpre (bf16 [M,64]) and dz = gout + dpre Wd (bf16; dz = NULL
+ * computes dpre only).
  * WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16). Weight/bias gradients: lc_gemm_tn.
  * Replaces: autograd of adapter.py:59-72. */
 int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,

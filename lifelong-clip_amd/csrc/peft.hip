@@ -341,6 +341,7 @@ int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, con
   int rc = lc_gemm_nt_ex(st, 10 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
                          AD_H, nullptr, 0, h, AD_H, ep);
   if (rc) return rc;
+  if (dz == nullptr) return LC_OK;  // dpre only (the input gradient is not needed)
   return lc_gemm_nt_ex(st, 11 /*EPI_AD_ADD*/, M, D, AD_H, dpre, AD_H, WdT, AD_H, nullptr, 1.0f, dz,
                        ldz, nullptr, 0, gout, ldg, ep);
 }

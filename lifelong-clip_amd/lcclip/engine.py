@@ -222,7 +222,7 @@ class BlockStack:
 
     # ------------------------------------------------------------------ backward
     def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None,
-                 grad_stream=None):
+                 grad_stream=None, need_dx: bool = True):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
         param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
         have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input.
@@ -230,7 +230,13 @@ class BlockStack:
         grad_stream: optional side HIP stream for the PEFT weight-gradient reductions (adapter
         dW/db, LoRA dA/dB), which feed only `grads`: they run beside the dX chain's MFMA-bound
         GEMMs. Each layer waits for the previous layer's side work before rewriting the shared
-        gradient buffers the side reads; sync_grads() joins it (done before returning)."""
+        gradient buffers the side reads; sync_grads() joins it (done before returning).
+
+        need_dx=False (a tower whose input is frozen: patch / token embeddings): nothing below
+        layer 0's first trainable parameter needs a gradient, so its out-proj dX, attention
+        backward, QKV dX and ln_1 backward are skipped, as the reference's autograd skips them
+        (adapter: all of them, dz included; LoRA: the attention backward stays for the in-proj
+        LoRA gradients). Returns (None, None) then."""
         M, D = dx.shape
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
@@ -260,32 +266,48 @@ class BlockStack:
             ops.layernorm_bwd(dh, s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight, dx_mid,
                               dx_midb, dres=dx)
             # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))
+            first = li == 0 and not need_dx
             if self.variant == "adapter":
-                dY = self._adapter_bwd(blk, st, dx_midb, s["hd1"], s["z1"], s["keep"], dz, grads)
+                dY = self._adapter_bwd(blk, st, dx_midb, s["hd1"], s["z1"], s["keep"],
+                                       None if first else dz, grads)
             else:
                 dY = dx_midb
+            if first and self.variant != "lora":
+                self._layer_done(li, grad_stream, on_layer)
+                break
             ops.gemm_nt(dY, st.woT, EPI_BF16, dO)
             attn = blk.attn
             if self.variant == "lora":
                 self._lora_grad(dY, s["O"], attn.out_proj.lora_A, attn.out_proj.lora_B,
                                 attn.scaling, grads, st.lora_out)
             ops.attn_bwd(s["qkv"], s["O"], dO, s["lse"], dqkv, n_seq, L, H, self.causal)
-            ops.gemm_nt(dqkv, st.wqkvT, EPI_BF16, dh)
             if self.variant == "lora":
                 self._lora_grad(dqkv, s["h1"], attn.in_proj_weight_lora_A,
                                 attn.in_proj_weight_lora_B, attn.scaling, grads, st.lora_in)
+            if first:
+                self._layer_done(li, grad_stream, on_layer)
+                break
+            ops.gemm_nt(dqkv, st.wqkvT, EPI_BF16, dh)
             ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
                               dxb_new, dres=dx_mid)
-            if grad_stream is not None:
-                ev = torch.cuda.Event()
-                ev.record(grad_stream)
-            if on_layer is not None:
-                on_layer(li)
+            ev = self._layer_done(li, grad_stream, on_layer)
             # ping-pong: the consumed output-gradient buffers are recycled for the next layer
             dx, dx_new = dx_new, dx
             dxb, dxb_new = dxb_new, dxb
         self.sync_grads()
+        if not need_dx:
+            return None, None
         return dx, dxb
+
+    @staticmethod
+    def _layer_done(li, grad_stream, on_layer):
+        ev = None
+        if grad_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(grad_stream)
+        if on_layer is not None:
+            on_layer(li)
+        return ev
 
     def sync_grads(self):
         """Make the current stream wait for the PEFT-gradient work on the side stream."""
@@ -313,7 +335,7 @@ class BlockStack:
         ad = blk.adaptmlp
         M = gout.shape[0]
         dpre = _empty((M, ad.down_size), BF16, gout.device)
-        ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz)
+        ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz)  # dz None: dpre only
         with self._side():
             if getattr(self, "_gs", None) is not None:
                 dpre.record_stream(self._gs)
@@ -415,7 +437,8 @@ class ImageTower:
         dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream)
+        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
+                            need_dx=False)
 
 
 class TextTower:
@@ -471,4 +494,4 @@ class TextTower:
         dxb = torch.zeros((C * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer)
+        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer, need_dx=False)

@@ -174,7 +174,8 @@ def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=N
 def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
     M, D = gout.shape
     call("lc_adapter_bwd", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
-         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz), dz.stride(0))
+         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz),
+         dz.stride(0) if dz is not None else D)
 
 
 def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
