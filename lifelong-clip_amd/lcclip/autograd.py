@@ -146,3 +146,33 @@ class _L2NormFn(torch.autograd.Function):
 
 def l2norm_apply(f):
     return _L2NormFn.apply(f)
+
+
+class _PromptTowerFn(torch.autograd.Function):
+    """Prompt-tuned image tower (models/mvp_clip.py:158-175, 256-262): the frozen blocks with
+    prompt tokens appended at the listed layers; gradients flow to the prompt tensors only."""
+
+    @staticmethod
+    def forward(ctx, tower, x0, n, L, training, save, layers, *prompts):
+        pd = {l: p.detach().contiguous().float() for l, p in zip(layers, prompts)}
+        f, c = tower.forward_embedded(x0, n, L, save, training, prompts=pd)
+        ctx.tower, ctx.saved_ctx, ctx.layers = tower, c, layers
+        return f
+
+    @staticmethod
+    def backward(ctx, df):
+        if ctx.saved_ctx is None:
+            raise RuntimeError("prompt tower forward ran without saving activations")
+        pg = {}
+        ctx.tower.backward(ctx.saved_ctx, df.contiguous().float(), {}, prompt_grads=pg)
+        ctx.saved_ctx = None
+        return (None, None, None, None, None, None, None, *[pg[l] for l in ctx.layers])
+
+
+def prompt_tower_apply(tower, transformer, x0, n, L, prompts: dict, training):
+    """prompts: {layer: [n, P, D]} (autograd-tracked). Returns image features [n, E]."""
+    _check_frozen(tower.stack)
+    layers = sorted(prompts)
+    ps = [prompts[l] for l in layers]
+    save = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
+    return _PromptTowerFn.apply(tower, x0, n, L, bool(training), save, layers, *ps)

@@ -158,71 +158,92 @@ class BlockStack:
         return old
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False):
-        """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None)."""
+    def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False, prompts=None,
+                stop=None):
+        """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None).
+
+        prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
+        before that layer and dropped after it (prompt tuning, models/mvp_clip.py:158-175: cat
+        along the sequence, block, x[:N]); that layer runs at L + P. stop: run layers [0, stop)
+        only (the MVP query pass, models/mvp_clip.py:211-216)."""
         self.stage()
         M, D = x.shape
         H = self.n_head
         dev = x.device
-        tmp_h = _empty((M, D), BF16, dev)
-        tmp_g = _empty((M, 4 * D), BF16, dev)
-        tmp_pre = None if save else _empty((M, 4 * D), BF16, dev)
+        P_of = {int(i): int(t.shape[1]) for i, t in (prompts or {}).items()}
+        Mmax = n_seq * (L + max(P_of.values(), default=0))
+        tmp_h = _empty((Mmax, D), BF16, dev)
+        tmp_g = _empty((Mmax, 4 * D), BF16, dev)
+        tmp_pre = None if save else _empty((Mmax, 4 * D), BF16, dev)
         saved = [] if save else None
-        for blk, st in zip(self.blocks, self.staged):
+        for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
+            if stop is not None and idx >= stop:
+                break
+            P = P_of.get(idx, 0)
+            Lx = L + P
+            Mx = n_seq * Lx
+            if P:
+                xe = _empty((Mx, D), F32, dev)
+                v = xe.view(n_seq, Lx, D)
+                v[:, :L] = x.view(n_seq, L, D)
+                v[:, L:] = prompts[idx]
+                x = xe
+            th = tmp_h[:Mx]
             s = {}
-            mean1 = _empty((M,), F32, dev)
-            rstd1 = _empty((M,), F32, dev)
-            h1 = _empty((M, D), BF16, dev) if (save and self.variant == "lora") else tmp_h
+            mean1 = _empty((Mx,), F32, dev)
+            rstd1 = _empty((Mx,), F32, dev)
+            h1 = _empty((Mx, D), BF16, dev) if (save and self.variant == "lora") else th
             ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
-            qkv = _empty((M, 3 * D), BF16, dev)
+            qkv = _empty((Mx, 3 * D), BF16, dev)
             ops.gemm_nt(h1, st.wqkv, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
-            O = _empty((M, D), BF16, dev)
-            lse = _empty((n_seq * H, L), F32, dev)
-            ops.attn_fwd(qkv, O, lse, n_seq, L, H, self.causal)
-            x_mid = _empty((M, D), F32, dev)
+            O = _empty((Mx, D), BF16, dev)
+            lse = _empty((n_seq * H, Lx), F32, dev)
+            ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
+            x_mid = _empty((Mx, D), F32, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 keep = 1.0 - ad.dropout if (training and ad.dropout > 0) else 1.0
                 seed1 = next(_seed_counter) * 0x9E3779B1
-                z1 = _empty((M, D), BF16, dev)
+                z1 = _empty((Mx, D), BF16, dev)
                 ops.gemm_nt(O, st.wo, EPI_BF16, z1, bias=blk.attn.out_proj.bias)
-                hd1 = _empty((M, ad.down_size), BF16, dev)
+                hd1 = _empty((Mx, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale, keep,
                                 seed1, x, x_mid, hd1, seed_dev=self.seed_dev)
                 s.update(z1=z1, hd1=hd1, keep=keep)
             else:
                 ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
-            mean2 = _empty((M,), F32, dev)
-            rstd2 = _empty((M,), F32, dev)
-            ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, tmp_h, mean2, rstd2)
-            pre = _empty((M, 4 * D), BF16, dev) if save else tmp_pre
+            mean2 = _empty((Mx,), F32, dev)
+            rstd2 = _empty((Mx,), F32, dev)
+            ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
+            pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
-            ops.gemm_nt(tmp_h, st.wfc, EPI_GELU_D if save else EPI_GELU, pre,
-                        bias=blk.mlp.c_fc.bias, out1=tmp_g)
-            x_out = _empty((M, D), F32, dev)
+            ops.gemm_nt(th, st.wfc, EPI_GELU_D if save else EPI_GELU, pre,
+                        bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
+            x_out = _empty((Mx, D), F32, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 seed2 = next(_seed_counter) * 0x9E3779B1
-                z2 = _empty((M, D), BF16, dev)
-                ops.gemm_nt(tmp_g, st.wpr, EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
-                hd2 = _empty((M, ad.down_size), BF16, dev)
+                z2 = _empty((Mx, D), BF16, dev)
+                ops.gemm_nt(tmp_g[:Mx], st.wpr, EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
+                hd2 = _empty((Mx, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
                                 s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
-                ops.gemm_nt(tmp_g, st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
+                ops.gemm_nt(tmp_g[:Mx], st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias,
+                            aux=x_mid)
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
-                         mean2=mean2, rstd2=rstd2, gd=pre)
+                         mean2=mean2, rstd2=rstd2, gd=pre, P=P)
                 if self.variant == "lora":
                     s["h1"] = h1
                 saved.append(s)
-            x = x_out
+            x = x_out if not P else x_out.view(n_seq, Lx, D)[:, :L].reshape(n_seq * L, D)
         return x, saved
 
     # ------------------------------------------------------------------ backward
     def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None,
-                 grad_stream=None, need_dx: bool = True):
+                 grad_stream=None, need_dx: bool = True, prompt_grads=None):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
         param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
         have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input.
@@ -236,68 +257,99 @@ class BlockStack:
         layer 0's first trainable parameter needs a gradient, so its out-proj dX, attention
         backward, QKV dX and ln_1 backward are skipped, as the reference's autograd skips them
         (adapter: all of them, dz included; LoRA: the attention backward stays for the in-proj
-        LoRA gradients). Returns (None, None) then."""
+        LoRA gradients). Returns (None, None) then.
+
+        prompt_grads: dict filled with {layer: f32 [n_seq, P, D]}, the gradient w.r.t. the
+        prompt tokens the forward appended at that layer (their rows of the layer's input
+        gradient; the dropped rows of its output carry zero gradient)."""
         M, D = dx.shape
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
         ev = None
         H = self.n_head
         dev = dx.device
-        da = _empty((M, 4 * D), BF16, dev)
-        dh = _empty((M, D), BF16, dev)
-        dO = _empty((M, D), BF16, dev)
-        dqkv = _empty((M, 3 * D), BF16, dev)
-        dz = _empty((M, D), BF16, dev) if self.variant == "adapter" else None
-        dx_mid = _empty((M, D), F32, dev)
-        dx_midb = _empty((M, D), BF16, dev)
-        dx_new = _empty((M, D), F32, dev)
-        dxb_new = _empty((M, D), BF16, dev)
+        Mmax = n_seq * (L + max((s.get("P", 0) for s in saved), default=0))
+        da = _empty((Mmax, 4 * D), BF16, dev)
+        dh = _empty((Mmax, D), BF16, dev)
+        dO = _empty((Mmax, D), BF16, dev)
+        dqkv = _empty((Mmax, 3 * D), BF16, dev)
+        dz = _empty((Mmax, D), BF16, dev) if self.variant == "adapter" else None
+        dx_mid = _empty((Mmax, D), F32, dev)
+        dx_midb = _empty((Mmax, D), BF16, dev)
+        # output-gradient buffers: the incoming pair and one more (ping-pong); prompt layers
+        # expand the current gradient into a free pair and compact their output back
+        pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev))]
+        cur = 0
         for li in range(len(self.blocks) - 1, -1, -1):
             blk, st, s = self.blocks[li], self.staged[li], saved[li]
             if ev is not None:
                 main.wait_event(ev)  # side reads of the buffers this layer rewrites are done
+            P = s.get("P", 0)
+            Lx = L + P
+            Mx = n_seq * Lx
+            if P:
+                if len(pairs) == 2:
+                    pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev)))
+                e = 2 if cur != 2 else 1
+                for src, dst in zip(pairs[cur], pairs[e]):
+                    v = dst[:Mx].view(n_seq, Lx, D)
+                    v[:, :L] = src[:M].view(n_seq, L, D)
+                    v[:, L:] = 0
+                cur = e
+            gx, gxb = pairs[cur][0][:Mx], pairs[cur][1][:Mx]
+            out = next(i for i in range(len(pairs)) if i != cur and (P == 0 or i != 0 or
+                                                                      pairs[0][0].shape[0] >= Mx))
+            ox, oxb = pairs[out][0][:Mx], pairs[out][1][:Mx]
             # ---- MLP sub-block: x_out = x_mid + [A](c_proj(gelu(c_fc(ln_2(x_mid)))))
             if self.variant == "adapter":
-                dY = self._adapter_bwd(blk, st, dxb, s["hd2"], s["z2"], s["keep"], dz, grads)
+                dY = self._adapter_bwd(blk, st, gxb, s["hd2"], s["z2"], s["keep"], dz[:Mx], grads)
             else:
-                dY = dxb
-            ops.gemm_nt(dY, st.wprT, EPI_MUL, da, aux=s["gd"])
-            ops.gemm_nt(da, st.wfcT, EPI_BF16, dh)
-            ops.layernorm_bwd(dh, s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight, dx_mid,
-                              dx_midb, dres=dx)
+                dY = gxb
+            ops.gemm_nt(dY, st.wprT, EPI_MUL, da[:Mx], aux=s["gd"])
+            ops.gemm_nt(da[:Mx], st.wfcT, EPI_BF16, dh[:Mx])
+            ops.layernorm_bwd(dh[:Mx], s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight,
+                              dx_mid[:Mx], dx_midb[:Mx], dres=gx)
             # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))
             first = li == 0 and not need_dx
             if self.variant == "adapter":
-                dY = self._adapter_bwd(blk, st, dx_midb, s["hd1"], s["z1"], s["keep"],
-                                       None if first else dz, grads)
+                dY = self._adapter_bwd(blk, st, dx_midb[:Mx], s["hd1"], s["z1"], s["keep"],
+                                       None if first else dz[:Mx], grads)
             else:
-                dY = dx_midb
+                dY = dx_midb[:Mx]
             if first and self.variant != "lora":
                 self._layer_done(li, grad_stream, on_layer)
                 break
-            ops.gemm_nt(dY, st.woT, EPI_BF16, dO)
+            ops.gemm_nt(dY, st.woT, EPI_BF16, dO[:Mx])
             attn = blk.attn
             if self.variant == "lora":
                 self._lora_grad(dY, s["O"], attn.out_proj.lora_A, attn.out_proj.lora_B,
                                 attn.scaling, grads, st.lora_out)
-            ops.attn_bwd(s["qkv"], s["O"], dO, s["lse"], dqkv, n_seq, L, H, self.causal)
+            ops.attn_bwd(s["qkv"], s["O"], dO[:Mx], s["lse"], dqkv[:Mx], n_seq, Lx, H, self.causal)
             if self.variant == "lora":
-                self._lora_grad(dqkv, s["h1"], attn.in_proj_weight_lora_A,
+                self._lora_grad(dqkv[:Mx], s["h1"], attn.in_proj_weight_lora_A,
                                 attn.in_proj_weight_lora_B, attn.scaling, grads, st.lora_in)
             if first:
                 self._layer_done(li, grad_stream, on_layer)
                 break
-            ops.gemm_nt(dqkv, st.wqkvT, EPI_BF16, dh)
-            ops.layernorm_bwd(dh, s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, dx_new,
-                              dxb_new, dres=dx_mid)
+            ops.gemm_nt(dqkv[:Mx], st.wqkvT, EPI_BF16, dh[:Mx])
+            ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
+                              oxb, dres=dx_mid[:Mx])
             ev = self._layer_done(li, grad_stream, on_layer)
-            # ping-pong: the consumed output-gradient buffers are recycled for the next layer
-            dx, dx_new = dx_new, dx
-            dxb, dxb_new = dxb_new, dxb
+            if P:
+                if ev is not None:
+                    main.wait_event(ev)  # the side stream read the expanded gradient
+                v = ox.view(n_seq, Lx, D)
+                if prompt_grads is not None:
+                    prompt_grads[li] = v[:, L:].clone()
+                # compact into the (consumed) expanded pair
+                pairs[cur][0][:M].view(n_seq, L, D).copy_(v[:, :L])
+                pairs[cur][1][:M].view(n_seq, L, D).copy_(oxb.view(n_seq, Lx, D)[:, :L])
+            else:
+                cur = out
         self.sync_grads()
         if not need_dx:
             return None, None
-        return dx, dxb
+        return pairs[cur][0][:M], pairs[cur][1][:M]
 
     @staticmethod
     def _layer_done(li, grad_stream, on_layer):
@@ -386,7 +438,8 @@ class ImageTower:
             ops.merge_weight(v.proj.detach(), None, None, 0.0, self.proj, self.projT)
             self._key = key
 
-    def forward(self, img, save: bool, training: bool = False):
+    def embed(self, img):
+        """conv1 + CLS/pos + ln_pre (model.py:756-766): (x0 f32 [n*L, D], n, L)."""
         v = self.visual
         self._stage()
         dev = img.device
@@ -413,18 +466,42 @@ class ImageTower:
         ops.vit_assemble(pe, v.class_embedding, v.positional_embedding, xa, n, npch)
         x0 = _empty((n * L, D), F32, dev)
         ops.layernorm_fwd(xa, v.ln_pre.weight, v.ln_pre.bias, x0)
-        x, saved = self.stack.forward(x0, n, L, save, training)
+        return x0, n, L
+
+    def _ln_post(self, x, n, L, out_dtype):
+        v = self.visual
+        dev = x.device
         cls_idx = torch.arange(n, device=dev, dtype=torch.int32) * L
-        lnp = _empty((n, D), BF16, dev)
+        lnp = _empty((n, v.width), out_dtype, dev)
         mean = _empty((n,), F32, dev)
         rstd = _empty((n,), F32, dev)
         ops.layernorm_fwd(x, v.ln_post.weight, v.ln_post.bias, lnp, mean, rstd, row_idx=cls_idx)
-        f = _empty((n, self.projT.shape[0]), F32, dev)
+        return lnp, cls_idx, mean, rstd
+
+    def query(self, x0, n, L, stop=None):
+        """The MVP key query (models/mvp_clip.py:196-218): blocks [0, stop) on x0 without
+        saving, then ln_post of the CLS rows (f32 [n, D], no projection)."""
+        x, _ = self.stack.forward(x0, n, L, save=False, stop=stop)
+        return self._ln_post(x, n, L, F32)[0]
+
+    def forward(self, img, save: bool, training: bool = False, prompts=None):
+        """img -> (features f32 [n, E], ctx). prompts: {layer: f32 [n, P, D]} appended before
+        that layer (prompt tuning, models/mvp_clip.py:158-175)."""
+        x0, n, L = self.embed(img)
+        return self.forward_embedded(x0, n, L, save, training, prompts)
+
+    def forward_embedded(self, x0, n, L, save: bool, training: bool = False, prompts=None):
+        """forward() from a precomputed embed() (the MVP query and prompt passes share x0)."""
+        self._stage()
+        x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts)
+        lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
+        f = _empty((n, self.projT.shape[0]), F32, x.device)
         ops.gemm_nt(lnp, self.projT, EPI_F32, f)
-        ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L) if save else None
+        ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L,
+                   prompt_layers=sorted(int(k) for k in (prompts or {}))) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads, on_layer=None, grad_stream=None):
+    def backward(self, ctx, df, grads, on_layer=None, grad_stream=None, prompt_grads=None):
         v = self.visual
         dev = df.device
         n, L = ctx["n"], ctx["L"]
@@ -437,8 +514,9 @@ class ImageTower:
         dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
+        # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
         self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
-                            need_dx=False)
+                            need_dx=0 in ctx["prompt_layers"], prompt_grads=prompt_grads)
 
 
 class TextTower:

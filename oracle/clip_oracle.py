@@ -26,6 +26,9 @@ refused by the environment, see SURVEY.md §8(c) and DESIGN.md §Oracle):
   * ``loss_on_probs``         methods/adapter_clip.py:88-89 + methods/_trainer.py:164
                               (CrossEntropyLoss applied to the probabilities — Q5)
   * ``adamw_step``            utils/train_utils.py:27-28 (torch.optim.AdamW, wd 1e-5)
+  * ``mvp_forward``           models/mvp_clip.py:158-291   (CLIP_MVP: no-grad key query,
+                              top-1 e-prompt / mask selection, prompt tuning with tokens
+                              appended per layer and dropped after it, masked logits)
 
 Parity pinning. The reference ships no tests, fixtures or golden vectors and could not be
 executed here, so the numeric restatement is pinned by the
@@ -471,3 +474,95 @@ def synthetic_state_dict(cfg: ClipConfig, method="vanilla", peft_encoder="none",
 TINY = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=2, vision_width=128,
                   vision_patch_size=16, context_length=77, vocab_size=512, transformer_width=64,
                   transformer_heads=1, transformer_layers=2)
+
+
+# ------------------------------------------------------------------------------------------------
+# MVP-CLIP (models/mvp_clip.py, BASELINE config 3): frozen vanilla backbone, prompt tuning.
+def mvp_embed(img, p, cfg: ClipConfig, rt=identity):
+    """conv1 + CLS/pos + ln_pre, batch-first [N, L, W] (mvp_clip.py:197-210 = model.py:756-766)."""
+    N = img.shape[0]
+    W, P = cfg.vision_width, cfg.vision_patch_size
+    g = cfg.grid
+    patches = img.reshape(N, 3, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(N, g * g, 3 * P * P)
+    x = linear(patches, p["visual.conv1.weight"].reshape(W, -1), None, rt)
+    cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
+    x = torch.cat([cls, x], dim=1) + p["visual.positional_embedding"]
+    return layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])
+
+
+def mvp_prompt_layers(g_prompt, e_prompt, pos_g, len_g, pos_e, len_e, n_layers):
+    """{layer: [B, P, W]} appended at that layer: g then e (mvp_clip.py:158-172; the prompt
+    tensors are viewed as [B, -1, len, W] and indexed by the layer's position in pos_*)."""
+    B, _, W = g_prompt.shape
+    g = g_prompt.reshape(B, -1, len_g, W)
+    e = e_prompt.reshape(B, -1, len_e, W)
+    out = {}
+    for n in range(n_layers):
+        parts = []
+        if n in pos_g:
+            parts.append(g[:, list(pos_g).index(n)])
+        if n in pos_e:
+            parts.append(e[:, list(pos_e).index(n)])
+        if parts:
+            out[n] = torch.cat(parts, dim=1)
+    return out
+
+
+def mvp_forward(img, tokens, p, cfg: ClipConfig, mvp: dict, pos_g=(0, 1), len_g=5,
+                pos_e=(2, 3, 4), len_e=20, use_last_layer=True, use_mask=True, rt=identity):
+    """CLIP_MVP.forward (mvp_clip.py:282-288) over forward_features (:182-264) and forward_head
+    (:266-280), prompt_func 'prompt_tuning', selection_size 1, use_contrastiv False.
+    mvp: {'key' [pool, W], 'mask' [pool, n_classes], 'g_prompts' [1, G, W], 'e_prompts'
+    [pool, E, W]}. Returns (logits [B, C] (masked when use_mask), similarity_loss, image
+    features [B, E], text features [C, E], mask [B, C], topk [B, 1])."""
+    vis, _ = tower_prefixes(cfg)
+    x0 = mvp_embed(img, p, cfg, rt)
+    B, N, W = x0.shape
+    with torch.no_grad():                                                       # :196-218
+        q = x0.clone()
+        stop = len(vis) if use_last_layer else len(vis) - 1
+        for pre in vis[:stop]:
+            q = block(q, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
+        query = layer_norm(q[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"])
+    distance = 1 - F.cosine_similarity(query.unsqueeze(1), mvp["key"], dim=-1)  # :224-225
+    topk = distance.topk(1, dim=1, largest=False)[1]                            # :231-232
+    distance = distance[torch.arange(B).unsqueeze(1), topk].squeeze(1)          # :233-235
+    e_prompts = mvp["e_prompts"][topk].squeeze(1)                               # :236
+    mask = mvp["mask"][topk].mean(1)                                            # :237
+    sim_loss = distance.mean()                                                  # :248
+    g_prompts = mvp["g_prompts"][0].repeat(B, 1, 1)                             # :250
+    prompts = mvp_prompt_layers(g_prompts, e_prompts, pos_g, len_g, pos_e, len_e, len(vis))
+    x = x0
+    for i, pre in enumerate(vis):                                               # :163-175
+        if i in prompts:
+            x = torch.cat([x, prompts[i]], dim=1)
+        x = block(x, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
+        x = x[:, :N]
+    x = rt(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
+    img_f = linear(x, p["visual.proj"].t(), None, rt)                          # :259-261
+    txt_f = encode_text(tokens, p, cfg, "vanilla", "none", rt)                   # :192
+    C = tokens.shape[0]
+    mask = torch.sigmoid(mask) * 2.0                                           # :263
+    logits, _, _ = clip_logits(img_f, txt_f, p["logit_scale"])                 # :266-280
+    if use_mask:
+        logits = logits * mask[:, :C]                                          # :286-287
+    return logits, sim_loss, img_f, txt_f, mask[:, :C], topk
+
+
+def mvp_params(cfg: ClipConfig, pool=10, n_classes=100, len_g=5, n_g=2, len_e=20, n_e=3, seed=7):
+    """MVP trainable tensors with the reference's shapes (mvp_clip.py:84-94): key randn,
+    mask zeros - 1 (here randomised around -1 so the mask gradient path is exercised),
+    g_prompts [1, n_g*len_g, W], e_prompts [pool, n_e*len_e, W] randn."""
+    g = torch.Generator().manual_seed(seed)
+    W = cfg.vision_width
+    return {
+        "key": torch.randn(pool, W, generator=g),
+        "mask": -1.0 + 0.5 * torch.randn(pool, n_classes, generator=g),
+        "g_prompts": torch.randn(1, n_g * len_g, W, generator=g),
+        "e_prompts": torch.randn(pool, n_e * len_e, W, generator=g),
+    }
+
+
+TINY_MVP = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=6, vision_width=128,
+                      vision_patch_size=16, context_length=77, vocab_size=512, transformer_width=64,
+                      transformer_heads=1, transformer_layers=2)

@@ -1,0 +1,139 @@
+"""MVP-CLIP (models/mvp_clip.py, BASELINE config 3) on the MI355X vs the CPU oracle
+(oracle.clip_oracle.mvp_forward): the prompt-tuned frozen image tower with tokens appended per
+layer (L + 5 at the g-prompt layers, L + 20 at the e-prompt layers), the no-grad key query,
+top-1 e-prompt / mask selection, masked logits, and the gradients of all four trainable tensors
+(key, mask, g_prompts, e_prompts) through loss_fn = CE + similarity loss.
+
+Parity unpinned against the reference itself (it cannot be run here); the
+oracle restatement is pinned by the identity test in tests/test_oracle.py (no prompt layers ==
+vanilla encode_image). Tolerances as tests/test_model_gpu.py: logits in cosine units < 2e-3 vs
+fp32 (< 1e-3 vs the bf16-rounding oracle), gradients rel-norm < 6e-2 vs fp32."""
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import clip_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def record(**kw):
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(root, "gpurun_out", "parity_metrics.jsonl"), "a") as f:
+        f.write(json.dumps(kw) + "\n")
+
+
+def build(cfg, sd, mv, dev, **kw):
+    from lcclip.mvp_clip import CLIP_MVP
+    m = CLIP_MVP.from_state_dict(sd, device=dev, num_classes=mv["mask"].shape[1],
+                                 task_num=mv["key"].shape[0], **kw)
+    with torch.no_grad():
+        for k in ("key", "mask", "g_prompts", "e_prompts"):
+            getattr(m, k).copy_(mv[k])
+    return m
+
+
+def oracle_grads(img, tok, y, sd, cfg, mv, **kw):
+    mvg = {k: v.clone().requires_grad_(True) for k, v in mv.items()}
+    logits, sim, *_ = o.mvp_forward(img, tok, sd, cfg, mvg, **kw)
+    loss = F.cross_entropy(logits, y) + sim                       # mvp_clip.py:290-291
+    loss.backward()
+    return loss.detach(), {k: v.grad for k, v in mvg.items()}
+
+
+@pytest.mark.parametrize("use_last_layer", [True, False])
+def test_mvp_tiny_forward_and_grads(dev, use_last_layer):
+    cfg = o.TINY_MVP
+    sd = o.synthetic_state_dict(cfg, seed=21)
+    mv = o.mvp_params(cfg, seed=3)
+    B, C = 3, 4
+    img = o.synthetic_images(B, cfg.image_resolution, seed=5)
+    tok = o.synthetic_tokens(C, cfg.context_length, seed=5, vocab=cfg.vocab_size)
+    y = torch.tensor([0, 3, 1])
+    with torch.no_grad():
+        l32, s32, i32, t32, m32, k32 = o.mvp_forward(img, tok, sd, cfg, mv,
+                                                     use_last_layer=use_last_layer)
+        l16, s16, *_ , k16 = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=use_last_layer,
+                                           rt=o.round_bf16)
+    loss_ref, g_ref = oracle_grads(img, tok, y, sd, cfg, mv, use_last_layer=use_last_layer)
+
+    m = build(cfg, sd, mv, dev, use_last_layer=use_last_layer)
+    m.train()
+    m.text_tokens = tok.to(dev)
+    logits = m(img.to(dev), tok.to(dev))
+    loss = m.loss_fn(logits, y.to(dev))
+    loss.backward()
+    torch.cuda.synchronize()
+    ls = math.exp(sd["logit_scale"].item())
+    met = dict(cos_err_vs_fp32=((logits.detach().cpu() - l32).abs().max() / ls).item(),
+               cos_err_vs_bf16=((logits.detach().cpu() - l16).abs().max() / ls).item(),
+               sim_abs=abs(m.get_similarity_loss().item() - s32.item()),
+               loss_abs=abs(loss.item() - loss_ref.item()))
+    for k in ("key", "mask", "g_prompts", "e_prompts"):
+        met[f"grad_{k}_rel"] = rel(getattr(m, k).grad, g_ref[k])
+    record(test="mvp_tiny", use_last_layer=use_last_layer, **met)
+    assert torch.equal(k16, k32)  # the oracle's own selection is stable under bf16 rounding
+    assert met["cos_err_vs_fp32"] < 2e-3 and met["cos_err_vs_bf16"] < 1e-3
+    assert met["sim_abs"] < 1e-3 and met["loss_abs"] < 5e-3
+    for k in ("key", "mask", "g_prompts", "e_prompts"):
+        assert met[f"grad_{k}_rel"] < 6e-2, (k, met)
+    # unselected e-prompt pools get exactly zero gradient; the count buffer saw B selections
+    sel = set(k32.flatten().tolist())
+    for j in range(mv["e_prompts"].shape[0]):
+        if j not in sel:
+            assert m.e_prompts.grad[j].abs().max().item() == 0.0
+    assert m.count.sum().item() == B
+    assert m.features.shape == (B, cfg.vision_width)
+
+
+def test_mvp_vit_b16_shapes(dev):
+    """Full ViT-B/16: 197 tokens, 202 at layers 0-1 and 217 at layers 2-4 (config 3's shapes),
+    B = 2, C = 4; forward vs the oracle in both rounding modes, prompt gradients vs fp32."""
+    cfg = o.VIT_B16
+    sd = o.synthetic_state_dict(cfg, seed=31)
+    mv = o.mvp_params(cfg, seed=4)
+    B, C = 2, 4
+    img = o.synthetic_images(B, 224, seed=2)
+    tok = o.synthetic_tokens(C, 77, seed=3)
+    y = torch.tensor([1, 2])
+    with torch.no_grad():
+        l32, s32, *_ = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=False)
+        l16, *_ = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=False, rt=o.round_bf16)
+    _, g_ref = oracle_grads(img, tok, y, sd, cfg, mv, use_last_layer=False)
+    m = build(cfg, sd, mv, dev, use_last_layer=False)
+    m.text_tokens = tok.to(dev)
+    logits = m(img.to(dev))
+    loss = m.loss_fn(logits, y.to(dev))
+    loss.backward()
+    torch.cuda.synchronize()
+    ls = math.exp(sd["logit_scale"].item())
+    met = dict(cos_err_vs_fp32=((logits.detach().cpu() - l32).abs().max() / ls).item(),
+               cos_err_vs_bf16=((logits.detach().cpu() - l16).abs().max() / ls).item())
+    for k in ("key", "mask", "g_prompts", "e_prompts"):
+        met[f"grad_{k}_rel"] = rel(getattr(m, k).grad, g_ref[k])
+    record(test="mvp_vit_b16", **met)
+    assert met["cos_err_vs_fp32"] < 2e-3 and met["cos_err_vs_bf16"] < 1e-3
+    for k in ("key", "mask", "g_prompts", "e_prompts"):
+        assert met[f"grad_{k}_rel"] < 6e-2, (k, met)
+
+
+def test_mvp_text_features_cached(dev):
+    cfg = o.TINY_MVP
+    m = build(cfg, o.synthetic_state_dict(cfg, seed=21), o.mvp_params(cfg), dev)
+    tok = o.synthetic_tokens(4, 77, seed=5, vocab=cfg.vocab_size).to(dev)
+    a = m.encode_text_cached(tok)
+    b = m.encode_text_cached(tok)
+    assert a is b
+    tok2 = tok.clone()
+    tok2[0, 2] = 7
+    assert not torch.equal(m.encode_text_cached(tok2), a)

@@ -204,3 +204,30 @@ def test_patchify_matches_conv1():
     conv = torch.nn.functional.conv2d(img, w, stride=16)  # [2, 8, 2, 2]
     gemm = o.patchify(img, 16) @ w.reshape(8, -1).t()     # [2*4, 8]
     assert torch.allclose(gemm, conv.permute(0, 2, 3, 1).reshape(8, 8), atol=1e-4)
+
+
+def test_mvp_oracle_pins():
+    """MVP restatement (mvp_clip.py:158-291): with no prompt layers the prompted tower is the
+    vanilla image tower (model.py:755-787) bit for bit; prompts appended at a layer change the
+    CLS output (the original tokens attend to them) while every layer keeps L rows; the
+    selected pool's mask row and e-prompts are the top-1 nearest key's."""
+    cfg = o.TINY_MVP
+    sd = o.synthetic_state_dict(cfg, seed=2)
+    mv = o.mvp_params(cfg, seed=1)
+    img = o.synthetic_images(3, cfg.image_resolution, seed=1)
+    tok = o.synthetic_tokens(2, cfg.context_length, seed=1, vocab=cfg.vocab_size)
+    with torch.no_grad():
+        none = o.mvp_forward(img, tok, sd, cfg, mv, pos_g=(), pos_e=())
+        full = o.mvp_forward(img, tok, sd, cfg, mv)
+        vanilla = o.encode_image(img, sd, cfg)
+    assert torch.equal(none[2], vanilla)
+    assert (full[2] - vanilla).abs().max() > 1e-3
+    # top-1 selection: the chosen key is the most cosine-similar one to the query
+    x0 = o.mvp_embed(img, sd, cfg)
+    q = x0
+    for pre in o.tower_prefixes(cfg)[0]:
+        q = o.block(q, sd, pre, cfg.vision_heads, False, "vanilla")
+    q = o.layer_norm(q[:, 0], sd["visual.ln_post.weight"], sd["visual.ln_post.bias"])
+    cos = torch.nn.functional.cosine_similarity(q.unsqueeze(1), mv["key"], dim=-1)
+    assert torch.equal(full[5].flatten(), cos.argmax(1))
+    assert torch.allclose(full[4], (torch.sigmoid(mv["mask"][cos.argmax(1)]) * 2)[:, :2])

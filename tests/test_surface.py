@@ -117,3 +117,24 @@ def test_ops_refuse_cpu_tensors():
     a = torch.zeros(64, 64, dtype=torch.bfloat16)
     with pytest.raises(LcError):
         ops.gemm_nt(a, a, ops.EPI_BF16, torch.zeros(64, 64, dtype=torch.bfloat16))
+
+
+def test_mvp_surface():
+    """CLIP_MVP keeps the reference's trainable set and shapes (mvp_clip.py:80-104): key
+    [pool, W], mask [pool, classes] = -1, g_prompts [1, 2*5, W], e_prompts [pool, 3*20, W];
+    the backbone frozen. ViT-B/16 defaults: 7680 + 1000 + 7680 + 460800 = 477 160 trainable."""
+    from lcclip.mvp_clip import CLIP_MVP
+    m = CLIP_MVP(model_name="tiny", arch_overrides=TINY_ARCH, device=None)
+    W = TINY_ARCH["vision_width"]
+    train = {n: tuple(p.shape) for n, p in m.named_parameters() if p.requires_grad}
+    assert train == {"key": (10, W), "mask": (10, 100), "g_prompts": (1, 10, W),
+                     "e_prompts": (10, 60, W)}
+    assert torch.equal(m.mask.detach(), -torch.ones(10, 100))
+    assert (m.g_size, m.e_size) == (10, 60)
+    n_b16 = 10 * 768 + 10 * 100 + m.g_size * 768 + 10 * m.e_size * 768
+    assert n_b16 == 477160
+    assert {n for n, _ in m.named_buffers()} >= {"pos_g_prompt", "pos_e_prompt", "similarity",
+                                                 "count"}
+    with pytest.raises(NotImplementedError):
+        CLIP_MVP(model_name="tiny", arch_overrides=TINY_ARCH, prompt_func="prefix_tuning",
+                 device=None).prefix_tuning(None, None, None)
