@@ -176,3 +176,76 @@ def prompt_tower_apply(tower, transformer, x0, n, L, prompts: dict, training):
     ps = [prompts[l] for l in layers]
     save = torch.is_grad_enabled() and any(p.requires_grad for p in ps)
     return _PromptTowerFn.apply(tower, x0, n, L, bool(training), save, layers, *ps)
+
+
+def _deep_grad(pg, layer, shape, like):
+    """Summed-over-sequences gradient of a replaced-row prompt; zero when the tower has no such
+    layer (the reference's counter never reaches that prompt, maple_clip/model.py:366)."""
+    g = pg.get(("R", layer))
+    return g.sum(0) if g is not None else torch.zeros(shape, dtype=F32, device=like.device)
+
+
+class _MapleTextFn(torch.autograd.Function):
+    """MaPLe TextEncoder (models/maple.py:40-61) on the engine: the learned input embeddings
+    x0 [C, L, D] and the deep text prompts replacing rows 1..n_ctx at layers 1.. (maple_clip
+    model.py:381-395). Gradients: d x0 (to ctx through autograd) and the deep prompts."""
+
+    @staticmethod
+    def forward(ctx, tower, tokens, training, save, x0, *deep):
+        C, L, D = x0.shape
+        replace = {i + 1: (1, d.detach().float().contiguous()) for i, d in enumerate(deep)}
+        f, c = tower.forward(tokens, save, training,
+                             x0=x0.detach().float().reshape(C * L, D).contiguous(),
+                             replace=replace)
+        ctx.tower, ctx.saved_ctx, ctx.shape, ctx.n_deep = tower, c, (C, L, D), len(deep)
+        ctx.deep_shapes = [tuple(d.shape) for d in deep]
+        return f
+
+    @staticmethod
+    def backward(ctx, df):
+        pg = {}
+        gx = ctx.tower.backward(ctx.saved_ctx, df.contiguous().float(), {}, prompt_grads=pg,
+                                need_dx=True)
+        ctx.saved_ctx = None
+        d_deep = [_deep_grad(pg, i + 1, ctx.deep_shapes[i], df) for i in range(ctx.n_deep)]
+        return (None, None, None, None, gx.view(*ctx.shape), *d_deep)
+
+
+class _MapleImageFn(torch.autograd.Function):
+    """MaPLe VisionTransformer_MaPLe.forward (maple_clip/model.py:551-590) on the engine: the
+    shared visual context appended before ln_pre, deep visual prompts replacing the last n_ctx
+    rows at layers 1.. (model.py:364-380)."""
+
+    @staticmethod
+    def forward(ctx, tower, img, training, save, shared, *deep):
+        keep = {}
+        x0, n, L = tower.embed(img, extra=shared, keep=keep if save else None)
+        P = shared.shape[0]
+        replace = {i + 1: (L - P, d.detach().float().contiguous()) for i, d in enumerate(deep)}
+        f, c = tower.forward_embedded(x0, n, L, save, training, replace=replace)
+        ctx.tower, ctx.saved_ctx, ctx.keep, ctx.P, ctx.n_deep = tower, c, keep, P, len(deep)
+        ctx.deep_shapes = [tuple(d.shape) for d in deep]
+        return f
+
+    @staticmethod
+    def backward(ctx, df):
+        pg = {}
+        gx = ctx.tower.backward(ctx.saved_ctx, df.contiguous().float(), {}, prompt_grads=pg,
+                                need_dx=True)
+        ctx.saved_ctx = None
+        L = ctx.keep["L"]
+        d_shared = ctx.tower.embed_backward(ctx.keep, gx, L - ctx.P)
+        d_deep = [_deep_grad(pg, i + 1, ctx.deep_shapes[i], df) for i in range(ctx.n_deep)]
+        return (None, None, None, None, d_shared, *d_deep)
+
+
+def maple_text_apply(tower, tokens, x0, deep, training):
+    _check_frozen(tower.stack)
+    save = torch.is_grad_enabled() and (x0.requires_grad or any(d.requires_grad for d in deep))
+    return _MapleTextFn.apply(tower, tokens, bool(training), save, x0, *deep)
+
+
+def maple_image_apply(tower, img, shared, deep, training):
+    _check_frozen(tower.stack)
+    save = torch.is_grad_enabled() and (shared.requires_grad or any(d.requires_grad for d in deep))
+    return _MapleImageFn.apply(tower, img, bool(training), save, shared, *deep)

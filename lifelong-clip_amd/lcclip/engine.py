@@ -159,13 +159,16 @@ class BlockStack:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False, prompts=None,
-                stop=None):
+                stop=None, replace=None):
         """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None).
 
         prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
         before that layer and dropped after it (prompt tuning, models/mvp_clip.py:158-175: cat
         along the sequence, block, x[:N]); that layer runs at L + P. stop: run layers [0, stop)
-        only (the MVP query pass, models/mvp_clip.py:211-216)."""
+        only (the MVP query pass, models/mvp_clip.py:211-216). replace: optional
+        {layer: (row, f32 [P, D] or [n_seq, P, D])} — rows [row, row + P) of every sequence are
+        overwritten before that layer (MaPLe's deep compound prompts,
+        models/maple_clip/model.py:352-395)."""
         self.stage()
         M, D = x.shape
         H = self.n_head
@@ -179,6 +182,11 @@ class BlockStack:
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
             if stop is not None and idx >= stop:
                 break
+            if replace and idx in replace:
+                r0, pr = replace[idx]
+                if idx == 0:
+                    x = x.clone()  # never write into the caller's input
+                x.view(n_seq, -1, D)[:, r0:r0 + pr.shape[-2]] = pr
             P = P_of.get(idx, 0)
             Lx = L + P
             Mx = n_seq * Lx
@@ -235,6 +243,8 @@ class BlockStack:
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
                          mean2=mean2, rstd2=rstd2, gd=pre, P=P)
+                if replace and idx in replace:
+                    s["R"] = (replace[idx][0], replace[idx][1].shape[-2])
                 if self.variant == "lora":
                     s["h1"] = h1
                 saved.append(s)
@@ -261,7 +271,9 @@ class BlockStack:
 
         prompt_grads: dict filled with {layer: f32 [n_seq, P, D]}, the gradient w.r.t. the
         prompt tokens the forward appended at that layer (their rows of the layer's input
-        gradient; the dropped rows of its output carry zero gradient)."""
+        gradient; the dropped rows of its output carry zero gradient), and {('R', layer):
+        f32 [n_seq, P, D]} for the rows the forward replaced there (those rows' input gradient,
+        which then stops: zeroed below that layer)."""
         M, D = dx.shape
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
@@ -335,6 +347,12 @@ class BlockStack:
             ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
                               oxb, dres=dx_mid[:Mx])
             ev = self._layer_done(li, grad_stream, on_layer)
+            if "R" in s:
+                r0, pr = s["R"]
+                if prompt_grads is not None:
+                    prompt_grads[("R", li)] = ox.view(n_seq, Lx, D)[:, r0:r0 + pr].clone()
+                ox.view(n_seq, Lx, D)[:, r0:r0 + pr] = 0
+                oxb.view(n_seq, Lx, D)[:, r0:r0 + pr] = 0
             if P:
                 if ev is not None:
                     main.wait_event(ev)  # the side stream read the expanded gradient
@@ -438,8 +456,12 @@ class ImageTower:
             ops.merge_weight(v.proj.detach(), None, None, 0.0, self.proj, self.projT)
             self._key = key
 
-    def embed(self, img):
-        """conv1 + CLS/pos + ln_pre (model.py:756-766): (x0 f32 [n*L, D], n, L)."""
+    def embed(self, img, extra=None, keep=None):
+        """conv1 + CLS/pos + ln_pre (model.py:756-766): (x0 f32 [n*L, D], n, L).
+        extra: optional f32 [P, D] rows appended to every sequence after the positional
+        embedding and before ln_pre (MaPLe's shared visual context,
+        models/maple_clip/model.py:566-575); L then counts them. keep: dict that receives what
+        embed_backward() needs."""
         v = self.visual
         self._stage()
         dev = img.device
@@ -464,9 +486,32 @@ class ImageTower:
         ops.gemm_nt(patches, self.conv_w, EPI_F32, pe)
         xa = _empty((n * L, D), F32, dev)
         ops.vit_assemble(pe, v.class_embedding, v.positional_embedding, xa, n, npch)
+        if extra is not None:
+            P = extra.shape[0]
+            xe = _empty((n * (L + P), D), F32, dev)
+            ve = xe.view(n, L + P, D)
+            ve[:, :L] = xa.view(n, L, D)
+            ve[:, L:] = extra.detach().float()
+            xa, L = xe, L + P
         x0 = _empty((n * L, D), F32, dev)
-        ops.layernorm_fwd(xa, v.ln_pre.weight, v.ln_pre.bias, x0)
+        mean = rstd = None
+        if keep is not None:
+            mean = _empty((n * L,), F32, dev)
+            rstd = _empty((n * L,), F32, dev)
+            keep.update(xa=xa, mean=mean, rstd=rstd, n=n, L=L)
+        ops.layernorm_fwd(xa, v.ln_pre.weight, v.ln_pre.bias, x0, mean, rstd)
         return x0, n, L
+
+    def embed_backward(self, keep, dx0, rows):
+        """Gradient w.r.t. the rows [rows, L) embed(extra=...) appended, summed over the
+        sequences: ln_pre backward of the input gradient dx0 f32 [n*L, D] (the rest of the
+        embedding is frozen)."""
+        v = self.visual
+        n, L = keep["n"], keep["L"]
+        D = v.width
+        dxa = _empty((n * L, D), F32, dx0.device)
+        ops.layernorm_bwd(dx0, keep["xa"], keep["mean"], keep["rstd"], v.ln_pre.weight, dxa, None)
+        return dxa.view(n, L, D)[:, rows:].sum(0)
 
     def _ln_post(self, x, n, L, out_dtype):
         v = self.visual
@@ -490,10 +535,11 @@ class ImageTower:
         x0, n, L = self.embed(img)
         return self.forward_embedded(x0, n, L, save, training, prompts)
 
-    def forward_embedded(self, x0, n, L, save: bool, training: bool = False, prompts=None):
+    def forward_embedded(self, x0, n, L, save: bool, training: bool = False, prompts=None,
+                         replace=None):
         """forward() from a precomputed embed() (the MVP query and prompt passes share x0)."""
         self._stage()
-        x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts)
+        x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts, replace=replace)
         lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
         f = _empty((n, self.projT.shape[0]), F32, x.device)
         ops.gemm_nt(lnp, self.projT, EPI_F32, f)
@@ -501,7 +547,9 @@ class ImageTower:
                    prompt_layers=sorted(int(k) for k in (prompts or {}))) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads, on_layer=None, grad_stream=None, prompt_grads=None):
+    def backward(self, ctx, df, grads, on_layer=None, grad_stream=None, prompt_grads=None,
+                 need_dx=False):
+        """Returns the stack-input gradient (f32 [n*L, D]) when need_dx, else None."""
         v = self.visual
         dev = df.device
         n, L = ctx["n"], ctx["L"]
@@ -515,8 +563,10 @@ class ImageTower:
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
-        self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
-                            need_dx=0 in ctx["prompt_layers"], prompt_grads=prompt_grads)
+        gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
+                                    need_dx=need_dx or 0 in ctx["prompt_layers"],
+                                    prompt_grads=prompt_grads)
+        return gx if need_dx else None
 
 
 class TextTower:
@@ -538,16 +588,21 @@ class TextTower:
             ops.merge_weight(P.detach(), None, None, 0.0, self.proj, self.projT)
             self._key = key
 
-    def forward(self, tokens, save: bool, training: bool = False):
+    def forward(self, tokens, save: bool, training: bool = False, x0=None, replace=None):
+        """tokens int64 [C, L] -> (features f32 [C, E], ctx). x0: optional precomputed input
+        embeddings f32 [C*L, D] (token + positional; MaPLe's learned context rows,
+        models/maple.py:40-45) — tokens then only locate the EOT rows; replace: row-replacing
+        prompts per layer (BlockStack.forward)."""
         c = self.clip
         self._stage()
         dev = tokens.device
         tokens = tokens.contiguous().to(torch.int64)
         C, L = tokens.shape
         D = c.transformer.width
-        x0 = _empty((C * L, D), F32, dev)
-        ops.text_embed(tokens, c.token_embedding.weight, c.positional_embedding, x0)
-        x, saved = self.stack.forward(x0, C, L, save, training)
+        if x0 is None:
+            x0 = _empty((C * L, D), F32, dev)
+            ops.text_embed(tokens, c.token_embedding.weight, c.positional_embedding, x0)
+        x, saved = self.stack.forward(x0, C, L, save, training, replace=replace)
         eot = _empty((C,), torch.int32, dev)
         ops.eot_rows(tokens, eot)
         lnf = _empty((C, D), BF16, dev)
@@ -559,7 +614,8 @@ class TextTower:
         ctx = dict(saved=saved, x=x, eot=eot, mean=mean, rstd=rstd, C=C, L=L) if save else None
         return f, ctx
 
-    def backward(self, ctx, df, grads, on_layer=None):
+    def backward(self, ctx, df, grads, on_layer=None, prompt_grads=None, need_dx=False):
+        """Returns the input-embedding gradient (f32 [C*L, D]) when need_dx, else None."""
         c = self.clip
         dev = df.device
         C, L = ctx["C"], ctx["L"]
@@ -572,4 +628,6 @@ class TextTower:
         dxb = torch.zeros((C * L, D), dtype=BF16, device=dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
-        self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer, need_dx=False)
+        gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer,
+                                    need_dx=need_dx, prompt_grads=prompt_grads)
+        return gx

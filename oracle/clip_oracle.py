@@ -29,6 +29,9 @@ refused by the environment, see SURVEY.md §8(c) and DESIGN.md §Oracle):
   * ``mvp_forward``           models/mvp_clip.py:158-291   (CLIP_MVP: no-grad key query,
                               top-1 e-prompt / mask selection, prompt tuning with tokens
                               appended per layer and dropped after it, masked logits)
+  * ``maple_forward``         models/maple.py:40-251 + models/maple_clip/model.py:316-401,
+                              551-590 (MaPLe: learned text context, shared visual context
+                              before ln_pre, deep prompts replacing rows at layers 1..2)
 
 Parity pinning. The reference ships no tests, fixtures or golden vectors and could not be
 executed here, so the numeric restatement is pinned by the
@@ -566,3 +569,80 @@ def mvp_params(cfg: ClipConfig, pool=10, n_classes=100, len_g=5, n_g=2, len_e=20
 TINY_MVP = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=6, vision_width=128,
                       vision_patch_size=16, context_length=77, vocab_size=512, transformer_width=64,
                       transformer_heads=1, transformer_layers=2)
+
+
+# ------------------------------------------------------------------------------------------------
+# MaPLe (models/maple.py + models/maple_clip/model.py, BASELINE config 5): frozen backbone,
+# multi-modal prompts. mp: {'ctx' [n_ctx, Dt], 'proj.weight' [Dv, Dt], 'proj.bias' [Dv],
+# 'text.{i}' [n_ctx, Dt], 'vproj.{i}.weight' [Dv, Dt], 'vproj.{i}.bias' [Dv]} for i < depth-1.
+def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, rt=identity):
+    """MaPLe.forward (maple.py:208-251) -> logits [B, C] (no softmax)."""
+    C = tokens.shape[0]
+    emb = p["token_embedding.weight"][tokens]                                  # maple.py:200-203
+    prefix, suffix = emb[:, :1], emb[:, 1 + n_ctx:]                            # :205-206
+    ctx = mp["ctx"].unsqueeze(0).expand(C, -1, -1)                             # :158-161
+    deep_text = [mp[f"text.{i}"] for i in range(depth - 1)]
+    deep_vis = [linear(mp[f"text.{i}"], mp[f"vproj.{i}.weight"], mp[f"vproj.{i}.bias"])
+                for i in range(depth - 1)]                                      # :164-169
+    shared = linear(mp["ctx"], mp["proj.weight"], mp["proj.bias"])              # :171-172
+    # text encoder (maple.py:53-68) with deep prompts at rows 1..n_ctx of layers 1..depth-1
+    # (maple_clip/model.py:381-395: prefix x[:1], context, suffix x[1 + n_ctx:])
+    x = torch.cat([prefix, ctx, suffix], dim=1) + p["positional_embedding"]     # :134-146, :54
+    _, txt = tower_prefixes(cfg)
+    for i, pre in enumerate(txt):
+        if 1 <= i <= len(deep_text):
+            x = torch.cat([x[:, :1], deep_text[i - 1].unsqueeze(0).expand(C, -1, -1),
+                           x[:, 1 + n_ctx:]], dim=1)
+        x = block(x, p, pre, cfg.transformer_heads, True, "vanilla", rt=rt)
+    x = x[torch.arange(C), tokens.argmax(dim=-1)]
+    x = rt(layer_norm(x, p["ln_final.weight"], p["ln_final.bias"]))
+    txt_f = linear(x, p["text_projection"].t(), None, rt)
+    # image encoder (maple_clip/model.py:551-590): shared context appended before ln_pre, deep
+    # prompts replacing the last n_ctx rows of layers 1..depth-1 (model.py:364-380)
+    N = img.shape[0]
+    W, P = cfg.vision_width, cfg.vision_patch_size
+    g = cfg.grid
+    patches = img.reshape(N, 3, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(N, g * g, 3 * P * P)
+    xi = linear(patches, p["visual.conv1.weight"].reshape(W, -1), None, rt)
+    cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
+    xi = torch.cat([cls, xi], dim=1) + p["visual.positional_embedding"]
+    xi = torch.cat([xi, shared.unsqueeze(0).expand(N, -1, -1)], dim=1)        # :568-570
+    xi = layer_norm(xi, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])    # :575
+    vis, _ = tower_prefixes(cfg)
+    for i, pre in enumerate(vis):
+        if 1 <= i <= len(deep_vis):
+            xi = torch.cat([xi[:, :-n_ctx], deep_vis[i - 1].unsqueeze(0).expand(N, -1, -1)], dim=1)
+        xi = block(xi, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
+    xi = rt(layer_norm(xi[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
+    img_f = linear(xi, p["visual.proj"].t(), None, rt)
+    logits, _, _ = clip_logits(img_f, txt_f, p["logit_scale"])                # :244-250
+    return logits
+
+
+def maple_params(cfg: ClipConfig, n_ctx=3, depth=3, seed=9):
+    """MaPLe prompt-learner tensors with the reference's shapes and init scales
+    (maple.py:94-123: ctx / compound text prompts N(0, 0.02); nn.Linear default init)."""
+    g = torch.Generator().manual_seed(seed)
+    Dt, Dv = cfg.transformer_width, cfg.vision_width
+    mp = {"ctx": 0.02 * torch.randn(n_ctx, Dt, generator=g),
+          "proj.weight": (Dt ** -0.5) * torch.randn(Dv, Dt, generator=g),
+          "proj.bias": 0.02 * torch.randn(Dv, generator=g)}
+    for i in range(depth - 1):
+        mp[f"text.{i}"] = 0.02 * torch.randn(n_ctx, Dt, generator=g)
+        mp[f"vproj.{i}.weight"] = (Dt ** -0.5) * torch.randn(Dv, Dt, generator=g)
+        mp[f"vproj.{i}.bias"] = 0.02 * torch.randn(Dv, generator=g)
+    return mp
+
+
+MAPLE_TO_MODULE = {"ctx": "prompt_learner.ctx", "proj.weight": "prompt_learner.proj.weight",
+                   "proj.bias": "prompt_learner.proj.bias",
+                   "text.0": "prompt_learner.compound_prompts_text.0",
+                   "text.1": "prompt_learner.compound_prompts_text.1",
+                   "vproj.0.weight": "prompt_learner.compound_prompt_projections.0.weight",
+                   "vproj.0.bias": "prompt_learner.compound_prompt_projections.0.bias",
+                   "vproj.1.weight": "prompt_learner.compound_prompt_projections.1.weight",
+                   "vproj.1.bias": "prompt_learner.compound_prompt_projections.1.bias"}
+
+TINY_MAPLE = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=4, vision_width=128,
+                        vision_patch_size=16, context_length=77, vocab_size=512,
+                        transformer_width=64, transformer_heads=1, transformer_layers=3)

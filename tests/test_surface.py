@@ -138,3 +138,25 @@ def test_mvp_surface():
     with pytest.raises(NotImplementedError):
         CLIP_MVP(model_name="tiny", arch_overrides=TINY_ARCH, prompt_func="prefix_tuning",
                  device=None).prefix_tuning(None, None, None)
+
+
+def test_maple_surface():
+    """MaPLe keeps the reference's trainable module tree (maple.py:64-123, 143-160): ctx,
+    proj, compound_prompts_text.{0,1}, compound_prompt_projections.{0,1}; backbone frozen."""
+    from lcclip.maple import MaPLe
+    m = MaPLe("tiny", arch_overrides=TINY_ARCH, device=None)
+    Dt, Dv = TINY_ARCH["transformer_width"], TINY_ARCH["vision_width"]
+    train = {n: tuple(p.shape) for n, p in m.named_parameters() if p.requires_grad}
+    assert train == {
+        "prompt_learner.ctx": (3, Dt),
+        "prompt_learner.proj.weight": (Dv, Dt), "prompt_learner.proj.bias": (Dv,),
+        "prompt_learner.compound_prompts_text.0": (3, Dt),
+        "prompt_learner.compound_prompts_text.1": (3, Dt),
+        "prompt_learner.compound_prompt_projections.0.weight": (Dv, Dt),
+        "prompt_learner.compound_prompt_projections.0.bias": (Dv,),
+        "prompt_learner.compound_prompt_projections.1.weight": (Dv, Dt),
+        "prompt_learner.compound_prompt_projections.1.bias": (Dv,)}
+    assert m.prompt_prefix == "X X X"  # the random-init branch without a tokenizer
+    ids = torch.tensor([[49406 % 512, 5, 6, 7, 8, 9, 511] + [0] * 70])
+    tok, pre, suf = m._split(ids)
+    assert pre.shape == (1, 1, Dt) and suf.shape == (1, 77 - 1 - 3, Dt)
