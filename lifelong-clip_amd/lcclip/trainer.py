@@ -108,13 +108,20 @@ class OnlineTrainer:
         if side is not None:
             side.wait_stream(main)
         tok_in = dp.shard_tokens(tokens) if self.shard_text else tokens
-        with torch.cuda.stream(side) if side is not None else _nullctx():
-            f_t, ct = self.txt.forward(tok_in, save=True, training=True)
+        cached = self._cached_text(tokens)
+        if cached is None:
+            train_t = bool(self.txt.stack.trainable_params())
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                f_t, ct = self.txt.forward(tok_in, save=train_t, training=True)
         f_i, ci = self.img.forward(images, save=True, training=True)
         if side is not None:
             main.wait_stream(side)
-        if self.shard_text:
-            f_t = dp.gather_rows(f_t, C).contiguous()
+        if cached is not None:
+            f_t, ct = cached, None
+        else:
+            if self.shard_text:
+                f_t = dp.gather_rows(f_t, C).contiguous()
+            self._store_text(tokens, f_t)
         B, E = f_i.shape
         img_n = torch.empty_like(f_i)
         txt_n = torch.empty_like(f_t)
@@ -148,6 +155,26 @@ class OnlineTrainer:
             main.wait_stream(side)
         dp.launch_bucket(self.flat_g, *self.txt_range)
         return loss, probs
+
+    # frozen text tower (peft_encoder 'image' / 'none'): its features depend only on the prompt
+    # tokens, so they are computed once per token tensor instead of every step
+    def _text_key(self, tokens):
+        if self.txt.stack.trainable_params() or torch.cuda.is_current_stream_capturing():
+            return None
+        c = self.clip
+        return (tokens.data_ptr(), tokens._version, tuple(tokens.shape),
+                tuple(p._version for p in c.transformer.parameters()),
+                c.token_embedding.weight._version, c.text_projection._version,
+                c.ln_final.weight._version)
+
+    def _cached_text(self, tokens):
+        key = self._text_key(tokens)
+        tc = getattr(self, "_txt_cache", None)
+        return tc[1] if (key is not None and tc is not None and tc[0] == key) else None
+
+    def _store_text(self, tokens, f_t):
+        key = self._text_key(tokens)
+        self._txt_cache = (key, f_t) if key is not None else None
 
     def _grad_stream(self, dev):
         if not self.overlap_grads:

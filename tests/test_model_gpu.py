@@ -252,3 +252,34 @@ def test_graph_replay_matches_eager(golden, dev, method):
     record(test="graph_vs_eager", method=method, param_delta_rel=r)
     assert r < 1e-3
     assert tg.ctr.tolist() == [3, 3]
+
+
+def test_online_evaluate_and_frozen_text_cache(golden, dev):
+    """methods/adapter_clip.py:132-175 over the HIP forward (argmax of the probabilities,
+    bucketed counts, confusion matrix), and the trainer's frozen-text cache: with
+    peft_encoder='image' the text features are computed once per token tensor and the step's
+    result equals the uncached one."""
+    from lcclip import OnlineTrainer
+    from lcclip.evaluate import online_evaluate
+    d, sd = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    w = make_wrapper(sd, "adapter", "both", dev)
+    w.set_token(tok)
+    res = online_evaluate(w, [(img, y), (img, y)], n_tasks=1)
+    with torch.no_grad():
+        pred = w(img)[0].argmax(-1)
+    acc = (pred == y).float().mean().item()
+    assert abs(res["avg_acc"] - acc) < 1e-6
+    assert sum(map(sum, res["confusion_matrix"])) == 2 * len(y)
+    # frozen text tower: cached features, same step result
+    sdi = o.synthetic_state_dict(o.TINY, "adapter", "image", seed=3)
+    t1 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))  # dropout 0: same masks
+    t2 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))
+    l1, p1 = t1.forward_backward(img, y, tok)
+    l1b, p1b = t1.forward_backward(img, y, tok)  # cache hit
+    t2._text_key = lambda tokens: None           # caching off
+    l2, p2 = t2.forward_backward(img, y, tok)
+    assert t1._txt_cache is not None
+    assert torch.equal(p1, p1b) and torch.equal(p1, p2) and torch.equal(l1, l2)
