@@ -855,7 +855,12 @@ int cu_count();
 void plan_tn(TnProb& p, int total_panels) {
   // measured (adapter dW, M = 50 432): one walker per CU 60 us; 2 per CU 80 us (twice the
   // partials to add atomically); contiguous per-walker chunks instead of block-cyclic 80-88 us
-  const int cus = cu_count();
+  static int walkers = -1;
+  if (walkers < 0) {
+    const char* e = getenv("LC_TN_WALKERS");
+    walkers = e ? atoi(e) : 0;
+  }
+  const int cus = walkers > 0 ? walkers : cu_count();
   const int nblk = (p.M + 63) / 64;
   int chunks = cus / total_panels;
   chunks = chunks < 1 ? 1 : chunks;

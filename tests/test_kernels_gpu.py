@@ -145,6 +145,30 @@ def test_gemm_splitk_tail(ops, dev, M, N, K):
     assert rel(o1, Ar.float() @ Br.float().t() + bias) < 4e-3
 
 
+def test_gemm_tail_rows_epilogues(ops, dev):
+    """N = 3072, K = 768 at M = 50 432 (c_fc fwd / c_proj dX, 2364 tiles = 9.23 rounds): the
+    two-output (QuickGELU, QuickGELU') and side-input (x aux) epilogues at full size, checked at
+    the first rows, across the 9-round boundary and in the last partial round, against torch."""
+    torch.manual_seed(3)
+    M, N, K = 50432, 3072, 768
+    A = torch.randn(M, K, device=dev).to(BF)
+    B = (torch.randn(N, K, device=dev) * K ** -0.5).to(BF)
+    bias = torch.randn(N, device=dev)
+    gd = torch.empty(M, N, device=dev, dtype=BF)
+    gl = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_GELU_D, gd, bias=bias, out1=gl)
+    aux = torch.randn(M, N, device=dev).to(BF)
+    om = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_MUL, om, alpha=0.5, aux=aux)
+    for lo, hi in ((0, 512), (49152 - 256, 49152 + 256), (M - 700, M)):
+        ref = A[lo:hi].float() @ B.float().t()
+        pre = ref + bias
+        sr = torch.sigmoid(1.702 * pre)
+        assert rel(gl[lo:hi], pre * sr) < 4e-3
+        assert rel(gd[lo:hi], sr + 1.702 * pre * sr * (1 - sr)) < 4e-3
+        assert rel(om[lo:hi], 0.5 * ref * aux[lo:hi].float()) < 4e-3
+
+
 @pytest.mark.parametrize("M,N1,N2", [(100, 128, 64), (3000, 64, 768), (50432 // 8, 768, 64)])
 def test_gemm_tn(ops, dev, M, N1, N2):
     torch.manual_seed(1)

@@ -6,7 +6,7 @@ Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 repo
 bytes of a wide coalesced streaming read, so read_bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB)
 is exact for 16-B-per-lane stores. Kernels are keyed by their short name and grid size (one
 entry per launch shape); the 'families' section aggregates the 256x256 ping-pong GEMM launches
-(gemm_pp_kernel<0|3|4>, the dominant kernel bench.py reports)."""
+(gemm_pp_kernel<EPI>, every epilogue, the dominant kernel bench.py reports)."""
 import collections
 import csv
 import glob
@@ -16,7 +16,9 @@ import sys
 
 
 def short(name):
-    base = name.split("(anonymous namespace)::")[-1]
+    """Kernel name without namespace, return type and parameter list (parameter types may
+    themselves be namespace-qualified, so cut at the first '(' after the name)."""
+    base = name.split("(anonymous namespace)::", 1)[-1] if "::" in name else name
     return base.split("(")[0]
 
 
