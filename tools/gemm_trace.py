@@ -31,8 +31,8 @@ for h in range(12):
     g1 = [d[256 + 4 * h + k] - t0 for k in range(4)]
     print(f"h={h:2d} G0 load {g0[0]:6d}->{g0[1]:6d} bar->{g0[2]:6d} comp->{g0[3]:6d} | "
           f"G1 load {g1[0]:6d}->{g1[1]:6d} bar->{g1[2]:6d} comp->{g1[3]:6d}")
-steps = [d[4 * h + 4] - d[4 * h] for h in range(40, 60)]
+steps = [d[4 * h + 4] - d[4 * h] for h in range(2, 20)]
 print("G0 cycles per half (steady state):", steps)
-print("G0 compute seg:", [d[4 * h + 3] - d[4 * h + 2] for h in range(40, 50)])
-print("G0 load seg (to reads done):", [d[4 * h + 1] - d[4 * h] for h in range(40, 50)])
-print("G0 wait+barrier:", [d[4 * h + 2] - d[4 * h + 1] for h in range(40, 50)])
+print("G0 compute seg:", [d[4 * h + 3] - d[4 * h + 2] for h in range(2, 12)])
+print("G0 load seg (to reads done):", [d[4 * h + 1] - d[4 * h] for h in range(2, 12)])
+print("G0 wait+barrier:", [d[4 * h + 2] - d[4 * h + 1] for h in range(2, 12)])
