@@ -68,7 +68,8 @@ int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* 
  * The environment variable LC_GEMM_TILE sets the initial value. */
 int lc_gemm_set_tile(int tile);
 
-/* Diagnostic: when p != NULL, the ping-pong GEMM stores s_memtime stamps of its segments
+/* Diagnostic (builds with -DLC_GEMM_TRACE only): when p != NULL, the ping-pong GEMM stores
+ * s_memtime stamps of its segments
  * (workgroup 0, waves 0 and 4) to p[512] (tools/gemm_trace.py). NULL disables (default). */
 int lc_gemm_set_debug(unsigned long long* p);
 

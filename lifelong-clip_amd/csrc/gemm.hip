@@ -429,6 +429,10 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 #pragma unroll
     for (int p = 0; p < PIECES; ++p) dma_piece(h, p);
   };
+  // segment timestamps for tools/gemm_trace.py / gemm_phases.py: compiled in only with
+  // -DLC_GEMM_TRACE (make TRACE=1) — even disabled, each stamp site costs an exec-masked branch
+  // inside the MFMA stream
+#ifdef LC_GEMM_TRACE
   const bool diag = ep.dbg != nullptr && blockIdx.x == 0 && (wave == 0 || wave == 4) && lane == 0;
   auto stamp = [&](int idx) {
     if (diag && idx < 256) {
@@ -437,6 +441,9 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
       ep.dbg[(wave / 4) * 256 + idx] = t;
     }
   };
+#else
+  auto stamp = [](int) {};
+#endif
 
   // prologue: halves 0..2 in flight; wait for this wave's part of half 0
   dma_half(0);

@@ -1,5 +1,6 @@
 """Diagnostic: prologue / main loop / epilogue of the ping-pong GEMM's workgroup 0 (s_memtime
-stamps, wave 0) for the step's shapes, with the launch's wall time for scale (dev tool)."""
+stamps, wave 0) for the step's shapes, with the launch's wall time for scale (dev tool).
+Needs a trace build: make -C lifelong-clip_amd/csrc TRACE=1."""
 import ctypes
 import os
 import sys

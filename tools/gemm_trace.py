@@ -1,4 +1,5 @@
-"""Diagnostic: segment timestamps of the ping-pong GEMM (block 0, waves 0 and 4)."""
+"""Diagnostic: segment timestamps of the ping-pong GEMM (block 0, waves 0 and 4).
+Needs a trace build: make -C lifelong-clip_amd/csrc TRACE=1 (the stamps are compiled out otherwise)."""
 import ctypes
 import os
 import sys
