@@ -77,30 +77,45 @@ head_rows_kernel(int B, int C, int E, const float* __restrict__ img_n,
 }
 
 // dF[r] = (dn - n (n.dn)) / norm[r],  dn[k] = s * sum_c dlog(r, c) * other[c][k] (+ dn_ext)
-// dlog(r, c) = dlogits[r*sr + c*sc]
+// dlog(r, c) = dlogits[r*sr + c*sc]. One workgroup per row r; the sum over c is spread over 8
+// groups of 32 lanes (c = cg, cg + 8, ...; lane kk owns k = kk + 32 j), so a row with many terms
+// (the text side: Co = batch) keeps 8 independent load streams in flight, and the 8 partial sums
+// meet in LDS in a fixed order (deterministic).
+constexpr int HFG_CG = 8;
 __global__ void __launch_bounds__(256)
 head_feat_grad_kernel(int R, int Co, int E, const float* __restrict__ dlogits, long sr, long sc,
                       const float* __restrict__ other_n, const float* __restrict__ self_n,
                       const float* __restrict__ norms, const float* __restrict__ logit_scale,
                       const float* __restrict__ dn_ext, float* __restrict__ dF) {
+  __shared__ float part_s[HFG_CG][1024];
   __shared__ float red[4];
   const int r = blockIdx.x, tid = threadIdx.x;
+  const int cg = tid >> 5, kk = tid & 31;
   const float s = __expf(*logit_scale);
-  float dn[4] = {0.f, 0.f, 0.f, 0.f};  // E <= 1024
-  for (int c = 0; c < Co; ++c) {
-    const float d = dlogits[(long)r * sr + (long)c * sc];
+  float acc[32];  // E <= 1024
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = tid + i * 256;
-      if (k < E) dn[i] += d * other_n[(long)c * E + k];
-    }
+  for (int j = 0; j < 32; ++j) acc[j] = 0.f;
+  for (int c = cg; c < Co; c += HFG_CG) {
+    const float d = dlogits[(long)r * sr + (long)c * sc];
+    const float* o = other_n + (long)c * E + kk;
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (kk + 32 * j < E) acc[j] += d * o[32 * j];
   }
+#pragma unroll
+  for (int j = 0; j < 32; ++j)
+    if (kk + 32 * j < E) part_s[cg][kk + 32 * j] = acc[j];
+  __syncthreads();
+  float dn[4] = {0.f, 0.f, 0.f, 0.f};
   float part = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = tid + i * 256;
     if (k < E) {
-      dn[i] *= s;
+      float v = 0.f;
+#pragma unroll
+      for (int g2 = 0; g2 < HFG_CG; ++g2) v += part_s[g2][k];
+      dn[i] = v * s;
       if (dn_ext) dn[i] += dn_ext[(long)r * E + k];
       part += dn[i] * self_n[(long)r * E + k];
     }
