@@ -104,6 +104,41 @@ class GemmTimer:
                     pp_flops=sum(f for _, f, _ in pp), pp_bytes=sum(b for _, _, b in pp))
 
 
+class TowerTimer:
+    """HIP events (torch's current stream, where the image tower launches) around the image
+    tower's forward and backward inside one step: the SURVEY §8(d) north-star ratio
+    B * F_img / (t_image_tower * peak), text tower and head excluded. The backward span ends
+    after the side-stream PEFT weight gradients have joined (they are image-tower work)."""
+
+    def __init__(self, tower):
+        self.tower = tower
+        self.spans = []
+
+    def __enter__(self):
+        self.fwd, self.bwd = self.tower.forward, self.tower.backward
+
+        def wrap(fn):
+            def timed(*a, **kw):
+                st = torch.cuda.current_stream()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                r = fn(*a, **kw)
+                e1.record(st)
+                self.spans.append((e0, e1))
+                return r
+            return timed
+        self.tower.forward, self.tower.backward = wrap(self.fwd), wrap(self.bwd)
+        return self
+
+    def __exit__(self, *a):
+        self.tower.forward, self.tower.backward = self.fwd, self.bwd
+
+    def ms(self):
+        torch.cuda.synchronize()
+        return sum(e0.elapsed_time(e1) for e0, e1 in self.spans)
+
+
 def pmc_traffic():
     """HBM bytes per ping-pong launch from the latest committed PMC summary
     (tools/profile_round.sh + tools/pmc_traffic.py), or None."""
@@ -234,6 +269,9 @@ def main():
     with GemmTimer(ops) as gt:
         trainer.eager_step(x, y, tok)
     gs = gt.summary()
+    with TowerTimer(trainer.img) as tt:
+        trainer.eager_step(x, y, tok)
+    img_ms = tt.ms()
     tf_stats = time_train_transform(B, dev)
 
     if rank == 0:
@@ -263,6 +301,12 @@ def main():
                        "launch": "hip_graph" if graph else "eager"},
             "images_per_s_per_gpu": round(total_ips / world, 2),
             "mfma_frac_step": round(f_step / (ms * 1e-3) / PEAK_BF16, 4),
+            "image_tower": {"ms_fwd_bwd": round(img_ms, 3),
+                            "tflops": round(B * f_img / (img_ms * 1e-3) / 1e12, 1),
+                            "mfma_frac": round(B * f_img / (img_ms * 1e-3) / PEAK_BF16, 4),
+                            "flops_per_image": f_img,
+                            "note": "SURVEY 8(d) north-star ratio: B*F_img / (t_image_tower * "
+                                    "peak), HIP events around the tower's fwd and bwd"},
             "roofline": {"bound": "mfma",
                          "kernel": "gemm_pp_kernel<EPI 0|6|7> (256x256 ping-pong bf16 MFMA GEMM: "
                                    "QKV, c_fc+QuickGELU+QuickGELU', c_proj fwd; QKV, c_fc, c_proj dX)",
