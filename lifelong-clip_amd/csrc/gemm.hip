@@ -20,6 +20,7 @@
 // runs are contiguous in (m, n) order and share A row-panels in its L2.
 #include "lc_common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 enum {
   EPI_BF16 = 0,        // out0 bf16 = acc*alpha + bias
@@ -552,6 +553,191 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 }
 
 // ---------------------------------------------------------------------------------------------
+// 4-wave 256x256 GEMM (one wave per SIMD, each wave a 128x128 sub-tile: 64 accumulator tiles in
+// AGPRs). K is consumed in 32-deep steps through a 4-slot LDS ring (slot = A [256][32] + B
+// [256][32] bf16 in 64-B rows, the ping-pong kernel's layout and swizzle); the DMA of step s+3 is
+// issued at step s, so every step has three steps of MFMA time to land. Per step: one barrier,
+// then the 16 fragment reads of step s+1 are issued ahead of step s's 64 MFMAs (fragments double-
+// buffered in VGPRs), so LDS latency hides behind the MFMA stream of the same wave.
+// Hazards: slot (s+3)%4 == (s-1)%4 was last read by fragment reads issued in step s-2 and waited
+// (lgkmcnt(0)) before the barrier of step s-1; step s+1's slot has landed for this wave (counted
+// vmcnt) and for every wave after the barrier of step s+1... the reads of step s+1 are issued
+// after the barrier of step s, which every wave passes only after its own DMA of step s+1 landed.
+template <int EPI>
+__global__ void __launch_bounds__(256, 1)
+gemm_w4_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
+               const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
+               float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
+               long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 2;
+  constexpr int TM = 8, TN = 8;
+  constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
+  constexpr int NSLOT = 4;
+  constexpr int PIECES = (BM + BN) / 16 / 4;  // 1-KiB DMA pieces per wave per step (8)
+  static_assert(PIECES == TM, "one DMA piece per MFMA row group");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int ns = K / 32;
+
+  // piece p of this wave = 16-row block p*4 + wave (A blocks 0..15, B blocks 16..31); source
+  // row pointers and LDS destinations computed once, a step only adds its k offset
+  const bf16_t* psrc[PIECES];
+  int pdst[PIECES];
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) {
+    const int blk = p * 4 + wave;
+    const bool isA = blk < BM / 16;
+    const int b = isA ? blk : blk - BM / 16;
+    const int r = b * 16 + (lane >> 2);
+    const int c = swz64(r, lane & 3);
+    const int rows_valid = isA ? M : N;
+    int gr = (isA ? m0 : n0) + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    psrc[p] = (isA ? A + (long)gr * lda : B + (long)gr * ldb) + c * 8;
+    pdst[p] = (isA ? 0 : BM * 64) + b * 1024;
+  }
+  auto dma_piece = [&](int s, int p) {
+    glds16(psrc[p] + s * 32, smem + (s % NSLOT) * SLOT + pdst[p]);
+  };
+  auto dma_step = [&](int s) {
+#pragma unroll
+    for (int p = 0; p < PIECES; ++p) dma_piece(s, p);
+  };
+  const int g = lane >> 4, t = lane & 15;
+  // fragment reads of the NEXT step as inline asm: the compiler does not track them, so it puts
+  // no lgkmcnt wait in front of this step's MFMAs; the explicit lgkmcnt(0) before the next
+  // step's barrier is what orders them (the registers are consumed one step later)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  uint32_t fa_off[TM], fb_off[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * (BM / WM) + i * 16 + t;
+    fa_off[i] = r * 64 + swz64(r, g) * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int r = wn * (BN / WN) + j * 16 + t;
+    fb_off[j] = BM * 64 + r * 64 + swz64(r, g) * 16;
+  }
+  auto read_frags = [&](int s, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) {
+    const uint32_t base = lds0 + (s % NSLOT) * SLOT;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(fa[i]) : "v"(base + fa_off[i]));
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      asm volatile("ds_read_b128 %0, %1" : "=v"(fb[j]) : "v"(base + fb_off[j]));
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: steps 0..2 in flight; step 0 landed everywhere; its fragments read
+  dma_step(0);
+  if (ns > 1) dma_step(1);
+  if (ns > 2) dma_step(2);
+  if (ns > 2) wait_vmcnt<2 * PIECES>();
+  else if (ns > 1) wait_vmcnt<PIECES>();
+  else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+  read_frags(0, fa0, fb0);
+
+  // accumulators pinned to AGPRs: the MFMA as inline asm with an "a" operand, so the compiler
+  // neither splits their live ranges nor shuffles them through VGPRs between steps
+  // one step: wait for step s+1 (own DMA), barrier, then step s's MFMAs with DMA s+3 and the
+  // fragment reads of s+1 (into the other buffer) interleaved
+#ifdef LC_GEMM_TRACE
+  const bool diag = ep.dbg != nullptr && blockIdx.x == 0 && lane == 0 && wave == 0;
+  auto stamp = [&](int idx) {
+    if (diag && idx < 512) {
+      unsigned long long tt;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt)::"memory");
+      ep.dbg[idx] = tt;
+    }
+  };
+#else
+  auto stamp = [](int) {};
+#endif
+  // FULL (std::true_type): steady state, s + 3 < ns, no per-group branches
+  auto step = [&](int s, auto full, const bf16x8 (&fa)[TM], const bf16x8 (&fb)[TN],
+                  bf16x8 (&na)[TM], bf16x8 (&nb)[TN]) {
+    constexpr bool FULL = decltype(full)::value;
+    stamp(3 * s);
+    if (FULL || s + 2 < ns) wait_vmcnt<PIECES>();  // s+1 landed; s+2 may fly
+    else if (s + 1 < ns) wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this step's fragments are in VGPRs
+    __builtin_amdgcn_s_barrier();
+    stamp(3 * s + 1);
+    // memory work spread through the MFMA stream: row group i of the 8x8 sub-tile grid carries
+    // DMA piece i of step s+3 and the A/B fragments i of step s+1 between its MFMAs, so the
+    // wave never queues 24 memory instructions in front of its matrix work
+#if defined(W4_NODMA)  // trace-only experiments: memory streams switched off (wrong results)
+    const bool dma = false, rd = FULL || s + 1 < ns;
+#elif defined(W4_NOREAD)
+    const bool dma = FULL || s + 3 < ns, rd = false;
+#else
+    const bool dma = FULL || s + 3 < ns, rd = FULL || s + 1 < ns;
+#endif
+    const uint32_t nbase = lds0 + ((s + 1) % NSLOT) * SLOT;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < TN / 2; ++j)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                     : "+a"(acc[i][j])
+                     : "v"(fb[j]), "v"(fa[i]));
+      if (dma) dma_piece(s + 3, i);
+      if (rd) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(na[i]) : "v"(nbase + fa_off[i]));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(nb[i]) : "v"(nbase + fb_off[i]));
+      }
+#pragma unroll
+      for (int j = TN / 2; j < TN; ++j)
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                     : "+a"(acc[i][j])
+                     : "v"(fb[j]), "v"(fa[i]));
+    }
+    stamp(3 * s + 2);
+  };
+  using Full = std::true_type;
+  using Tail = std::false_type;
+  int s = 0;
+  for (; s + 4 < ns; s += 2) {
+    step(s, Full{}, fa0, fb0, fa1, fb1);
+    step(s + 1, Full{}, fa1, fb1, fa0, fb0);
+  }
+  // at most four steps remain (s even)
+  if (s < ns) step(s, Tail{}, fa0, fb0, fa1, fb1);
+  if (s + 1 < ns) step(s + 1, Tail{}, fa1, fb1, fa0, fb0);
+  if (s + 2 < ns) step(s + 2, Tail{}, fa0, fb0, fa1, fb1);
+  if (s + 3 < ns) step(s + 3, Tail{}, fa1, fb1, fa0, fb0);
+  // the last MFMA results reach the AGPRs before the epilogue reads them (asm MFMAs are opaque
+  // to the hazard recognizer)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave done with the ring: the epilogue reuses it
+  store_tile<BM, BN, WM, WN, EPI>(acc, smem, NSLOT * SLOT, m0, n0, M, bias, alpha, out0, ldo0,
+                                  out1, ldo1, aux, ldaux, ep);
+}
+
+// ---------------------------------------------------------------------------------------------
 // TN split-K GEMM: C[N1,N2] += alpha * sum_m A[m][n1] * B[m][n2].
 // 64x64 output tile per workgroup, 4 waves (2x2, 32x32 each), K-step = 64 rows of M staged
 // row-major in LDS and read TRANSPOSED with ds_read_b64_tr_b16 (4 rows x 16 cols per 16-lane
@@ -949,6 +1135,29 @@ SplitK plan_split(int tiles, int K, void* ws, long ws_bytes) {
   return sk;
 }
 
+int launch_w4(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
+              const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  dim3 grid(tiles), block(256);
+#define LC_W4_CASE(E)                                                                          \
+  case E:                                                                                      \
+    hipLaunchKernelGGL((gemm_w4_kernel<E>), grid, block, 0, st, M, N, K, A, lda, B, ldb, bias, \
+                       alpha, o0, l0, o1, l1, aux, la, ep);                                    \
+    break;
+  switch (epi) {
+    LC_W4_CASE(EPI_BF16)
+    LC_W4_CASE(EPI_F32)
+    LC_W4_CASE(EPI_RESID)
+    LC_W4_CASE(EPI_GELU_D)
+    LC_W4_CASE(EPI_MUL)
+    default:
+      return LC_EINVAL;
+  }
+#undef LC_W4_CASE
+  LC_LAUNCH_RET();
+}
+
 int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
               void* o1, long l1, const void* aux, long la, const EpiParams& ep, void* ws,
@@ -1020,7 +1229,8 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     else if (M >= 4096 && N % 256 == 0 && (N >= 2048 || K >= 2048)) tile = 5;
     else tile = 1;
   }
-  if (((tile == 3 || tile == 5 || tile == 6) && N % 256) || ((tile == 1 || tile == 2) && N % 128))
+  if (((tile == 3 || tile == 5 || tile == 6 || tile == 7) && N % 256) ||
+      ((tile == 1 || tile == 2) && N % 128))
     tile = 4;
   switch (tile) {
     case 1:
@@ -1032,6 +1242,9 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     case 3:
       return launch_nt<256, 256, 2, 4, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                           ldo0, out1, ldo1, aux, ldaux, ep);
+    case 7:
+      return launch_w4(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                       aux, ldaux, ep);
     case 5:
     case 6:
       return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
@@ -1068,7 +1281,7 @@ int lc_gemm_set_debug(unsigned long long* p) {
 }
 
 int lc_gemm_set_tile(int tile) {
-  LC_CHECK_ARG(tile >= 0 && tile <= 6);
+  LC_CHECK_ARG(tile >= 0 && tile <= 7);
   g_force_tile = tile;
   return LC_OK;
 }
