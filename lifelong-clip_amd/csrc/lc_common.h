@@ -22,8 +22,12 @@ LC_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return *reinterpret_cast<bf16_t*>(&b);
 }
+// Two values in one v_cvt_pk_bf16_f32. (Two scalar f2bf + shift/or made hipcc convert pairs in
+// its own order and re-shuffle the halves: 2-3 extra VALU per pair in every bf16 epilogue.)
+typedef float lc_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 lc_bf16x2 __attribute__((ext_vector_type(2)));
 LC_DEV uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((lc_f32x2){lo, hi}, lc_bf16x2));
 }
 
 LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
