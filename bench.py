@@ -54,10 +54,13 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
     return x, tok.to(dev), y.to(dev)
 
 
-def routes_to_pp(M, N, K):
+def routes_to_pp(M, N, K, epi):
     """The lc_gemm_nt tile selector's rule for the 256x256 ping-pong kernel (gemm.hip,
-    lc_gemm_nt_ex): the dominant kernel of the step."""
-    return N % 128 == 0 and M >= 4096 and N % 256 == 0 and (N >= 2048 or K >= 2048)
+    lc_gemm_nt_ex): the dominant kernel of the step. The c_proj dX x QuickGELU' GEMM (EPI_MUL,
+    K <= 1024) goes to the 4-wave kernel instead."""
+    pp = N % 128 == 0 and M >= 4096 and N % 256 == 0 and (N >= 2048 or K >= 2048)
+    from lcclip.ops import EPI_MUL
+    return pp and not (epi == EPI_MUL and K <= 1024)
 
 
 class GemmTimer:
@@ -86,7 +89,7 @@ class GemmTimer:
                 t = kw.get(extra)
                 if t is not None:
                     nbytes += t.numel() * t.element_size()
-            self.records.append((e0, e1, 2.0 * M * N * K, nbytes, routes_to_pp(M, N, K)))
+            self.records.append((e0, e1, 2.0 * M * N * K, nbytes, routes_to_pp(M, N, K, epi)))
             return r
         self.ops.gemm_nt = timed
         import lcclip.engine as eng
@@ -308,8 +311,8 @@ def main():
                             "note": "SURVEY 8(d) north-star ratio: B*F_img / (t_image_tower * "
                                     "peak), HIP events around the tower's fwd and bwd"},
             "roofline": {"bound": "mfma",
-                         "kernel": "gemm_pp_kernel<EPI 0|6|7> (256x256 ping-pong bf16 MFMA GEMM: "
-                                   "QKV, c_fc+QuickGELU+QuickGELU', c_proj fwd; QKV, c_fc, c_proj dX)",
+                         "kernel": "gemm_pp_kernel<EPI 0|6> (256x256 ping-pong bf16 MFMA GEMM: "
+                                   "QKV, c_fc+QuickGELU+QuickGELU', c_proj fwd; QKV, c_fc dX)",
                          "achieved": round(achieved / 1e12, 2), "peak": PEAK_BF16 / 1e12,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4),
                          "traffic": None if traffic is None else round(traffic),

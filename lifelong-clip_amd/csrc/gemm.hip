@@ -1228,6 +1228,8 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     if (N % 128 != 0) tile = 4;
     else if (M >= 4096 && N % 256 == 0 && (N >= 2048 || K >= 2048)) tile = 5;
     else tile = 1;
+    // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 298 vs 315 us (bench_gemm.py)
+    if (tile == 5 && epi == EPI_MUL && K <= 1024) tile = 7;
   }
   if (((tile == 3 || tile == 5 || tile == 6 || tile == 7) && N % 256) ||
       ((tile == 1 || tile == 2) && N % 128))
