@@ -1,0 +1,38 @@
+"""Adapter weight-gradient microbenchmark (dev tool): lc_adapter_wgrad (dWu, dbu, dWd, dbd in one
+gemm_tn_wide launch) at the ViT-B/16 step shape M = 50 432, D = 768; HIP-event timing, algorithmic
+bytes (gout, z, h, dpre read once) / time. LC_TN_WALKERS overrides the walkers per launch."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "lifelong-clip_amd")]
+import torch  # noqa: E402
+
+from lcclip import _lib, ops  # noqa: E402
+
+if os.environ.get("LCLIB"):  # an experimental build of the library
+    _lib.load(os.path.join(ROOT, os.environ["LCLIB"]))
+
+dev = torch.device("cuda:0")
+M, D = int(os.environ.get("M", 50432)), 768
+g = torch.randn(M, D, device=dev).to(torch.bfloat16)
+z = torch.randn(M, D, device=dev).to(torch.bfloat16)
+h = torch.randn(M, 64, device=dev).to(torch.bfloat16)
+dp = torch.randn(M, 64, device=dev).to(torch.bfloat16)
+dWu = torch.zeros(D, 64, device=dev)
+dWd = torch.zeros(64, D, device=dev)
+dbu = torch.zeros(D, device=dev)
+dbd = torch.zeros(64, device=dev)
+for _ in range(3):
+    ops.adapter_wgrad(g, h, z, dp, 0.1, dWu, dbu, dWd, dbd)
+reps = 20
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(reps):
+    ops.adapter_wgrad(g, h, z, dp, 0.1, dWu, dbu, dWd, dbd)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) / reps * 1e3
+nbytes = (g.numel() + z.numel() + h.numel() + dp.numel()) * 2
+print(f"walkers={os.environ.get('LC_TN_WALKERS', 'cu')} M={M}: {us:.1f} us  "
+      f"{nbytes / us / 1e3:.0f} GB/s", flush=True)
