@@ -95,6 +95,9 @@ head_feat_grad_kernel(int R, int Co, int E, const float* __restrict__ dlogits, l
   float acc[32];  // E <= 1024
 #pragma unroll
   for (int j = 0; j < 32; ++j) acc[j] = 0.f;
+  // unrolled so that several rows' loads are in flight per lane (the FMA order per acc is
+  // unchanged: the result is bit-identical to the rolled loop)
+#pragma unroll 4
   for (int c = cg; c < Co; c += HFG_CG) {
     const float d = dlogits[(long)r * sr + (long)c * sc];
     const float* o = other_n + (long)c * E + kk;

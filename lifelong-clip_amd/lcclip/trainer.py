@@ -138,15 +138,21 @@ class OnlineTrainer:
         lo, hi, per = dp.prompt_slice(C) if self.shard_text else (0, C, C)
         d_tp = torch.zeros(per * dp.world if self.shard_text else C, E, dtype=F32, device=dev)
         ops.head_feat_grad(dlog, C, 1, txt_n, img_n, ni, self.logit_scale, d_i)
-        ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
         train_txt = ct is not None and bool(self.txt.stack.trainable_params())
-        w_dt = dp.sum_async(d_tp) if (self.shard_text and train_txt) else None
+        # dL/dT (a sum over the batch per prompt) is only needed by the text backward: unless it
+        # is all-reduced first, it is computed on the text stream, off the image chain
+        w_dt = None
+        if self.shard_text and train_txt:
+            ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
+            w_dt = dp.sum_async(d_tp)
         if train_txt:
             if side is not None:
                 side.wait_stream(main)
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 if w_dt is not None:
                     w_dt.wait()  # makes the text stream wait for the dL/dT all-reduce
+                else:
+                    ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
                 self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
         if self.img.stack.trainable_params():
             self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook(),
