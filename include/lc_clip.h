@@ -148,6 +148,16 @@ int lc_cast_bf16(hipStream_t stream, long n, const float* src, void* dst);
 int lc_merge_weight(hipStream_t stream, int N, int K, int r, const float* W, const float* A,
                     const float* B, float scaling, void* out, void* outT);
 
+/* Batched plain casts: out[i] = bf16(W[i]) ([N[i], K[i]]) and, when outT[i] != NULL, the
+ * transposed copy [K[i], N[i]], for n <= LC_CAST_MAX matrices in one launch (host arrays of
+ * device pointers). Used for the adapter weights after every optimizer step.
+ * Replaces: the per-call fp32 -> half weight casts autocast performs inside F.linear for the
+ * adapter's down/up projections (adapter.py:11-72 under the autocast at
+ * methods/adapter_clip.py:87). */
+#define LC_CAST_MAX 64
+int lc_cast_weights_bf16(hipStream_t stream, int n, const float* const* W, const int* N,
+                         const int* K, void* const* out, void* const* outT);
+
 /* dB[N,r] += scaling * dY^T (X A^T);  dA[r,K] += scaling * (dY B)^T X   (r == 4).
  * Replaces: autograd of the two F.linear LoRA products (lora.py:838-839, 1073-1074). */
 int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,

@@ -31,15 +31,13 @@ __global__ void cast_bf16_kernel(long n, const float* __restrict__ src, bf16_t* 
 // LDS once, each thread 4 rows x 4 columns (float4 loads of W, 8-byte bf16 stores), and the
 // transposed copy written from an LDS tile as 4 consecutive columns per store.
 constexpr int MERGE_RMAX = 8;
-__global__ void __launch_bounds__(256)
-merge_kernel(int N, int K, int r, const float* __restrict__ W, const float* __restrict__ A,
-             const float* __restrict__ B, float s, bf16_t* __restrict__ out,
-             bf16_t* __restrict__ outT) {
+LC_DEV void merge_tile(int N, int K, int r, const float* __restrict__ W, const float* __restrict__ A,
+                       const float* __restrict__ B, float s, bf16_t* __restrict__ out,
+                       bf16_t* __restrict__ outT, int n0, int k0) {
   __shared__ float tile[64][65];
   __shared__ float As[MERGE_RMAX][64];
   __shared__ float Bs[64][MERGE_RMAX];
   const int tid = threadIdx.x;
-  const int n0 = blockIdx.y * 64, k0 = blockIdx.x * 64;
   for (int i = tid; i < r * 64; i += 256) {
     const int j = i / 64, kk = i % 64;
     As[j][kk] = (k0 + kk < K) ? A[(long)j * K + k0 + kk] : 0.f;
@@ -101,6 +99,31 @@ merge_kernel(int N, int K, int r, const float* __restrict__ W, const float* __re
         if (nb + c < N) outT[(long)k * N + nb + c] = f2bf(tcol[(nt0 + c) * 65]);
     }
   }
+}
+
+__global__ void __launch_bounds__(256)
+merge_kernel(int N, int K, int r, const float* __restrict__ W, const float* __restrict__ A,
+             const float* __restrict__ B, float s, bf16_t* __restrict__ out,
+             bf16_t* __restrict__ outT) {
+  merge_tile(N, K, r, W, A, B, s, out, outT, blockIdx.y * 64, blockIdx.x * 64);
+}
+
+// Many plain casts in one launch (the adapter weights of every block after each optimizer step:
+// 2 x 2 small matrices per block, 48 launches of ~5 us each on the step's critical path before).
+// blockIdx.y = item, blockIdx.x = 64x64 tile of that item.
+struct CastBatch {
+  const float* W[LC_CAST_MAX];
+  bf16_t* out[LC_CAST_MAX];
+  bf16_t* outT[LC_CAST_MAX];
+  int N[LC_CAST_MAX], K[LC_CAST_MAX];
+};
+__global__ void __launch_bounds__(256) cast_batch_kernel(CastBatch b) {
+  const int it = blockIdx.y;
+  const int N = b.N[it], K = b.K[it];
+  const int tk = (K + 63) / 64;
+  if ((int)blockIdx.x >= tk * ((N + 63) / 64)) return;
+  merge_tile(N, K, 0, b.W[it], nullptr, nullptr, 0.f, b.out[it], b.outT[it],
+             (blockIdx.x / tk) * 64, (blockIdx.x % tk) * 64);
 }
 
 // ---------------------------------------------------------------------------- LoRA gradients
@@ -294,6 +317,26 @@ int lc_merge_weight(hipStream_t st, int N, int K, int r, const float* W, const f
   dim3 grid((K + 63) / 64, (N + 63) / 64);
   hipLaunchKernelGGL(merge_kernel, grid, dim3(256), 0, st, N, K, r, W, A, B, scaling,
                      (bf16_t*)out, (bf16_t*)outT);
+  LC_LAUNCH_RET();
+}
+
+int lc_cast_weights_bf16(hipStream_t st, int n, const float* const* W, const int* N,
+                         const int* K, void* const* out, void* const* outT) {
+  LC_CHECK_ARG(n >= 0 && n <= LC_CAST_MAX && (n == 0 || (W && N && K && out && outT)));
+  if (n == 0) return LC_OK;
+  CastBatch b{};
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    LC_CHECK_ARG(W[i] != nullptr && out[i] != nullptr && N[i] > 0 && K[i] > 0);
+    b.W[i] = W[i];
+    b.out[i] = static_cast<bf16_t*>(out[i]);
+    b.outT[i] = static_cast<bf16_t*>(outT[i]);
+    b.N[i] = N[i];
+    b.K[i] = K[i];
+    const int t = ((N[i] + 63) / 64) * ((K[i] + 63) / 64);
+    tiles = t > tiles ? t : tiles;
+  }
+  hipLaunchKernelGGL(cast_batch_kernel, dim3(tiles, n), dim3(256), 0, st, b);
   LC_LAUNCH_RET();
 }
 

@@ -37,6 +37,7 @@ SIGNATURES = {
                            P, c_int, c_int, c_int, P],
     "lc_cast_bf16": [P, c_long, P, P],
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
+    "lc_cast_weights_bf16": [P, c_int, P, P, P, P, P],
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
     "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
                        P, c_long, P],

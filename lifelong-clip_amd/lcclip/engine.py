@@ -90,6 +90,7 @@ class BlockStack:
             st.peft_key = None
 
     def stage(self):
+        casts = []
         for blk, st in zip(self.blocks, self.staged):
             attn, mlp = blk.attn, blk.mlp
             fkey = _key(attn.in_proj_weight, attn.out_proj.weight, mlp.c_fc.weight, mlp.c_proj.weight)
@@ -137,9 +138,12 @@ class BlockStack:
                     st.wdT = _empty((D, H), BF16, dev)
                     st.wu = _empty((D, H), BF16, dev)
                     st.wuT = _empty((H, D), BF16, dev)
-                    ops.merge_weight(ad.down_proj.weight.detach(), None, None, 0.0, st.wd, st.wdT)
-                    ops.merge_weight(ad.up_proj.weight.detach(), None, None, 0.0, st.wu, st.wuT)
+                    casts.append((ad.down_proj.weight.detach(), st.wd, st.wdT))
+                    casts.append((ad.up_proj.weight.detach(), st.wu, st.wuT))
                     st.peft_key = pkey
+        # the adapter weights of every block change at each optimizer step: one launch for all
+        if casts:
+            ops.cast_weights(casts)
 
     @staticmethod
     def _stage_lora(st, name, A, B):

@@ -157,6 +157,29 @@ def merge_weight(W, A, B, scaling, out, outT=None):
     return out
 
 
+CAST_MAX = 64  # LC_CAST_MAX
+
+
+def cast_weights(items):
+    """items: [(W f32 [N, K], out bf16 [N, K], outT bf16 [K, N] or None)] -> one launch per
+    CAST_MAX items (lc_cast_weights_bf16)."""
+    import ctypes
+    for i in range(0, len(items), CAST_MAX):
+        chunk = items[i:i + CAST_MAX]
+        n = len(chunk)
+        for W, out, outT in chunk:
+            if W.dtype != F32 or not W.is_contiguous() or out.dtype != BF16 or not out.is_contiguous():
+                raise ValueError("cast_weights: W must be contiguous f32, out contiguous bf16")
+            if out.shape != W.shape or (outT is not None and outT.shape != W.shape[::-1]):
+                raise ValueError("cast_weights: shape mismatch")
+        ws = (ctypes.c_void_p * n)(*[ptr(W) for W, _, _ in chunk])
+        Ns = (ctypes.c_int * n)(*[W.shape[0] for W, _, _ in chunk])
+        Ks = (ctypes.c_int * n)(*[W.shape[1] for W, _, _ in chunk])
+        outs = (ctypes.c_void_p * n)(*[ptr(o) for _, o, _ in chunk])
+        outTs = (ctypes.c_void_p * n)(*[ptr(t) for _, _, t in chunk])
+        call("lc_cast_weights_bf16", stream_of(chunk[0][0]), n, ws, Ns, Ks, outs, outTs)
+
+
 def lora_grad(dY, X, A, B, scaling, dA, dB):
     M, N = dY.shape
     K = X.shape[1]

@@ -521,3 +521,22 @@ def test_head_fused_and_module_kernels(ops, dev, B, C):
     dl = torch.empty(B, C, device=dev)
     ops.softmax_bwd_rows(pr, dp, dl)
     assert rel(dl, pr * (dp - (pr * dp).sum(-1, keepdim=True))) < 1e-5
+
+
+def test_cast_weights_batch(ops, dev):
+    """lc_cast_weights_bf16: several matrices (ragged shapes, with and without the transposed
+    copy) in one launch, bit-equal to torch's round-to-nearest-even bf16 cast."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    shapes = [(64, 768), (768, 64), (5, 130), (129, 3), (64, 512)]
+    items = []
+    for i, (n, k) in enumerate(shapes):
+        W = torch.randn(n, k, device=dev, generator=g)
+        out = torch.empty(n, k, device=dev, dtype=BF)
+        outT = torch.empty(k, n, device=dev, dtype=BF) if i % 2 == 0 else None
+        items.append((W, out, outT))
+    ops.cast_weights(items)
+    torch.cuda.synchronize()
+    for W, out, outT in items:
+        assert torch.equal(out, W.to(BF))
+        if outT is not None:
+            assert torch.equal(outT, W.t().to(BF))
