@@ -11,6 +11,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "lifelong-clip_amd")]
 import torch  # noqa: E402
 
 from lcclip import _lib, ops  # noqa: E402
+
+if os.environ.get("LCLIB"):  # an experimental build of the library
+    _lib.load(os.path.join(ROOT, os.environ["LCLIB"]))
 from lcclip._lib import call, ptr, stream_of  # noqa: E402
 
 M = int(os.environ.get("M", 50432))
