@@ -1,0 +1,7 @@
+source gpu_step.sh
+# same-box A/B: the committed HEAD (worktree exp_head/, built in place) vs the working tree
+for i in 1 2; do
+  run head$i 200 python -u exp_head/bench.py --steps 20 --warmup 5 --no-cpu-baseline
+  run new$i 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
+done
+echo done
