@@ -1230,6 +1230,10 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 298 vs 315 us (bench_gemm.py)
     if (tile == 5 && epi == EPI_MUL && K <= 1024) tile = 7;
+    // one-k-tile streams (adapter up-projection / input gradient, K = 64): 128x64 tiles keep
+    // more rows in flight per CU (tools/bench_adapter_kernels.py: AD_UP 83 -> 77 us, AD_ADD
+    // 37 -> 35 us)
+    if (K <= 64) tile = 4;
   }
   if (((tile == 3 || tile == 5 || tile == 6 || tile == 7) && N % 256) ||
       ((tile == 1 || tile == 2) && N % 128))
