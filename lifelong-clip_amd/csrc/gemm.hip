@@ -265,7 +265,10 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
   constexpr int TN = BN / WN / 16;  // 16-col subtiles per wave (output features)
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int LOADS = (BM + BN) / 8 / NW;  // glds instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
+  // the epilogue stages PASS rows of each wave's accumulator tile through the same LDS
+  constexpr int EPI_BYTES = NW * ((BM / WM) % 32 == 0 ? 32 : 16) * (BN / WN + 4) * 4;
+  constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -295,21 +298,7 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     stage_tile<BN, NW>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
   };
 
-  // prologue: STAGES-1 tiles in flight, wait for the first
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s, s);
-  if (nk >= STAGES - 1) wait_vmcnt<LOADS * (STAGES - 2)>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int pre = kt + STAGES - 1;
-    int pbuf = cur + STAGES - 1;
-    if (pbuf >= STAGES) pbuf -= STAGES;
-    if (pre < nk) stage(pbuf, pre);
-    const char* sa = smem + cur * STAGE_BYTES;
+  auto compute = [&](const char* sa) {
     const char* sb = sa + BM * 128;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -326,15 +315,44 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
-    // tile kt+1 must have landed; tiles up to kt+STAGES-1 may stay in flight
-    if (pre < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
+  };
+
+  if constexpr (STAGES == 1) {
+    // one LDS stage (the one-k-tile streams, K = 64: more workgroups per CU); the closing
+    // barrier of a tile also guards the next tile's DMA and the epilogue's reuse of the LDS
+    for (int kt = 0; kt < nk; ++kt) {
+      stage(0, kt);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      compute(smem);
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    // prologue: STAGES-1 tiles in flight, wait for the first
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nk) stage(s, s);
+    if (nk >= STAGES - 1) wait_vmcnt<LOADS * (STAGES - 2)>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    cur = cur + 1 == STAGES ? 0 : cur + 1;
+
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int pre = kt + STAGES - 1;
+      int pbuf = cur + STAGES - 1;
+      if (pbuf >= STAGES) pbuf -= STAGES;
+      if (pre < nk) stage(pbuf, pre);
+      compute(smem + cur * STAGE_BYTES);
+      // tile kt+1 must have landed; tiles up to kt+STAGES-1 may stay in flight
+      if (pre < nk) wait_vmcnt<LOADS * (STAGES - 2)>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+    }
   }
 
-  store_tile<BM, BN, WM, WN, EPI>(acc, smem, STAGES * STAGE_BYTES, m0, n0, M, bias, alpha, out0,
-                                  ldo0, out1, ldo1, aux, ldaux, ep);
+  store_tile<BM, BN, WM, WN, EPI>(acc, smem, SMEM, m0, n0, M, bias, alpha, out0, ldo0, out1,
+                                  ldo1, aux, ldaux, ep);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1233,7 +1251,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     // one-k-tile streams (adapter up-projection / input gradient, K = 64): 128x64 tiles keep
     // more rows in flight per CU (tools/bench_adapter_kernels.py: AD_UP 83 -> 77 us, AD_ADD
     // 37 -> 35 us)
-    if (K <= 64) tile = 4;
+    if (K <= 64) tile = 11;
   }
   if (((tile == 3 || tile == 5 || tile == 6 || tile == 7) && N % 256) ||
       ((tile == 1 || tile == 2) && N % 128))
@@ -1255,6 +1273,9 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     case 6:
       return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                        aux, ldaux, ep, ws, ws_bytes);
+    case 11:  // 128x64, one LDS stage
+      return launch_nt<128, 64, 4, 1, 1>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
+                                         ldo0, out1, ldo1, aux, ldaux, ep);
     default:
       return launch_nt<128, 64, 4, 1, 2>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                          ldo0, out1, ldo1, aux, ldaux, ep);
@@ -1287,7 +1308,7 @@ int lc_gemm_set_debug(unsigned long long* p) {
 }
 
 int lc_gemm_set_tile(int tile) {
-  LC_CHECK_ARG(tile >= 0 && tile <= 7);
+  LC_CHECK_ARG(tile >= 0 && tile <= 11);
   g_force_tile = tile;
   return LC_OK;
 }

@@ -36,7 +36,7 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 11])
 def test_gemm_nt_every_tile_exact(ops, dev, tile):
     """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
     the fused QuickGELU-derivative epilogue against torch at bf16 tolerance."""
