@@ -76,7 +76,7 @@ LC_DEV void wait_vmcnt() {
 
 // Epilogue shared by the GEMM kernels: acc holds the swapped MFMA layout (lane: 4 consecutive
 // columns n of one row m per 16x16 subtile).
-template <int BM, int BN, int WM, int WN, int EPI, int TM, int TN>
+template <int BM, int BN, int WM, int WN, int EPI, int PASS_MAX = 32, int TM, int TN>
 LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0, int n0, int M,
                        const float* __restrict__ bias, float alpha, void* __restrict__ out0,
                        long ldo0, void* __restrict__ out1, long ldo1, const void* __restrict__ aux,
@@ -89,7 +89,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   // of its accumulator tile in the (now idle) stage ring and reads them back row-contiguous:
   // every global load/store of the epilogue covers whole 256-B row segments.
   constexpr int WT_M = BM / WM, WT_N = BN / WN;
-  constexpr int PASS = (WT_M % 32 == 0) ? 32 : 16;
+  constexpr int PASS = (WT_M % PASS_MAX == 0) ? PASS_MAX : 16;
   constexpr int LSTR = WT_N + 4;          // floats per staged row (pad: bank spread)
   // columns per lane on the read-back: 8 when every output is bf16 (one 16-B store per lane and
   // output: half the store instructions of 4 columns — the epilogue tail is store-issue bound),
@@ -266,7 +266,9 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
   constexpr int STAGE_BYTES = (BM + BN) * 128;
   constexpr int LOADS = (BM + BN) / 8 / NW;  // glds instructions per wave per stage
   // the epilogue stages PASS rows of each wave's accumulator tile through the same LDS
-  constexpr int EPI_BYTES = NW * ((BM / WM) % 32 == 0 ? 32 : 16) * (BN / WN + 4) * 4;
+  // (16-row passes for the one-stage variant: half the staging LDS and prefetch registers)
+  constexpr int PASS_MAX = STAGES == 1 ? 16 : 32;
+  constexpr int EPI_BYTES = NW * ((BM / WM) % PASS_MAX == 0 ? PASS_MAX : 16) * (BN / WN + 4) * 4;
   constexpr int SMEM = STAGES * STAGE_BYTES > EPI_BYTES ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -351,8 +353,8 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     }
   }
 
-  store_tile<BM, BN, WM, WN, EPI>(acc, smem, SMEM, m0, n0, M, bias, alpha, out0, ldo0, out1,
-                                  ldo1, aux, ldaux, ep);
+  store_tile<BM, BN, WM, WN, EPI, PASS_MAX>(acc, smem, SMEM, m0, n0, M, bias, alpha, out0, ldo0,
+                                            out1, ldo1, aux, ldaux, ep);
 }
 
 // ---------------------------------------------------------------------------------------------
