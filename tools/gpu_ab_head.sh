@@ -1,5 +1,6 @@
 source gpu_step.sh
-# same-box A/B: the committed HEAD (worktree exp_head/, built in place) vs the working tree
+# same-box A/B: the committed HEAD vs the working tree. Set up first (and remove afterwards):
+#   git worktree add exp_head HEAD && make -C exp_head/lifelong-clip_amd/csrc -j8
 run tests 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q --timeout 120 --timeout-method thread
 run adk 100 python -u tools/bench_adapter_kernels.py
 for i in 1 2; do
