@@ -205,12 +205,19 @@ int lc_adamw(hipStream_t stream, long n, float* p, const float* g, float* m, flo
  * captured step graph advances on every replay. */
 int lc_counter_add(hipStream_t stream, int n, long long* ctr, long long delta);
 
+/* *ctr += 1 unless *skip != 0 (skip may be NULL): the AdamW step counter, which advances only
+ * for applied updates — GradScaler.step skips optimizer.step() on inf/NaN gradients, so torch's
+ * state['step'] stays (methods/adapter_clip.py:94-95). Feeds lc_adamw's step_dev. */
+int lc_adam_step_advance(hipStream_t stream, long long* ctr, const int* skip);
+
 /* out[r] = f[r] / ||f[r]||, norms[r] = ||f[r]||   (model.py:966-969, adapter_clip.py:78). */
 int lc_l2norm_rows(hipStream_t stream, int R, int E, const float* f, long ldf, float* out,
                    float* norms);
 
 /* Head forward+backward: logits = exp(*logit_scale) img_n txt_n^T, probs = softmax(logits),
  * *loss += mean_b CE(probs_b, labels_b), dlogits = d loss / d logits. *loss must be zeroed.
+ * A label outside [0, C) makes *loss and that row of dlogits NaN (so lc_check_finite skips
+ * the update) — torch's CrossEntropyLoss raises on it.
  * Replaces: model.py:972-973, models/adapter_clip.py:99, methods/adapter_clip.py:88-89. */
 int lc_clip_head(hipStream_t stream, int B, int C, int E, const float* img_n, const float* txt_n,
                  const float* logit_scale, const int64_t* labels, float* probs, float* dlogits,

@@ -58,8 +58,17 @@ head_rows_kernel(int B, int C, int E, const float* __restrict__ img_n,
     z2 += __expf(p);
   }
   z2 = wave_sum(z2);
-  const int y = (int)labels[b];
+  const int64_t y64 = labels[b];
   const float invB = 1.0f / B;
+  if (y64 < 0 || y64 >= C) {
+    // a label outside the class list (e.g. remapped against a rank-local list): poison the loss
+    // and this row's gradient, so the non-finite check skips the update instead of training on
+    // garbage (torch's CrossEntropyLoss raises here)
+    for (int c = lane; c < C; c += 64) dlogits[(long)b * C + c] = __builtin_nanf("");
+    if (lane == 0) atomicAdd(loss, __builtin_nanf(""));
+    return;
+  }
+  const int y = (int)y64;
   // dL/dp_c = (softmax(p)_c - [c == y]) / B ; dL/dlogit = p * (dp - sum p*dp)
   float dot = 0.f;
   for (int c = lane; c < C; c += 64) {

@@ -293,6 +293,13 @@ __global__ void counter_add_kernel(int n, long long* ctr, long long delta) {
   if ((int)threadIdx.x < n) ctr[threadIdx.x] += delta;
 }
 
+// AdamW's state['step'] advances only when the update is applied: GradScaler.step skips
+// optimizer.step() on non-finite gradients (methods/adapter_clip.py:94), so torch's counter
+// does not move either.
+__global__ void step_advance_kernel(long long* ctr, const int* skip) {
+  if (threadIdx.x == 0 && !(skip && *skip)) *ctr += 1;
+}
+
 int grid_for(long work, int block) {
   long gsz = (work + block - 1) / block;
   if (gsz > 4096) gsz = 4096;
@@ -411,6 +418,12 @@ int lc_adamw(hipStream_t st, long n, float* p, const float* g, float* m, float* 
 int lc_counter_add(hipStream_t st, int n, long long* ctr, long long delta) {
   LC_CHECK_ARG(n > 0 && n <= 64 && ctr != nullptr);
   hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, st, n, ctr, delta);
+  LC_LAUNCH_RET();
+}
+
+int lc_adam_step_advance(hipStream_t st, long long* ctr, const int* skip) {
+  LC_CHECK_ARG(ctr != nullptr);
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st, ctr, skip);
   LC_LAUNCH_RET();
 }
 

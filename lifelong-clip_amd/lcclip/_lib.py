@@ -46,6 +46,7 @@ SIGNATURES = {
     "lc_check_finite": [P, c_long, P, P],
     "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P, P],
     "lc_counter_add": [P, c_int, P, c_long],
+    "lc_adam_step_advance": [P, P, P],
     "lc_l2norm_rows": [P, c_int, c_int, P, c_long, P, P],
     "lc_clip_head": [P, c_int, c_int, c_int, P, P, P, P, P, P, P],
     "lc_head_logits": [P, c_int, c_int, c_int, P, P, P, P, P],

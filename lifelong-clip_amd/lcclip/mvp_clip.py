@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from . import autograd as lc_autograd
 from . import clip_loader
 from .adapter_clip import EOT_TOKEN, SOT_TOKEN
+from .textcache import TokenFeatureCache
 
 
 class CLIP_MVP(nn.Module):
@@ -87,7 +88,7 @@ class CLIP_MVP(nn.Module):
         self.g_prompts = nn.Parameter(torch.randn(g_pool, self.g_size, embed_dim))
         self.e_prompts = nn.Parameter(torch.randn(e_pool, self.e_size, embed_dim))
         self.exposed_classes = 0
-        self._txt_cache = None
+        self._txt_cache = TokenFeatureCache()
         if device is not None and str(device) != "cpu":
             self.to(device)
 
@@ -129,14 +130,17 @@ class CLIP_MVP(nn.Module):
 
     def encode_text_cached(self, text_tokens):
         """backbone.encode_text (mvp_clip.py:192) for the frozen text tower, cached on the token
-        tensor's identity/version and the text weights' versions."""
+        content and the text weights' versions (lcclip.textcache)."""
         tt = self.backbone
-        key = (text_tokens.data_ptr(), text_tokens._version, tuple(text_tokens.shape),
-               tt.token_embedding.weight._version, tt.text_projection._version)
-        if self._txt_cache is None or self._txt_cache[0] != key:
+        key = (tuple(p._version for p in tt.transformer.parameters()),
+               tt.token_embedding.weight._version, tt.text_projection._version,
+               tt.ln_final.weight._version)
+        f = self._txt_cache.get(text_tokens, key)
+        if f is None:
             with torch.no_grad():
-                self._txt_cache = (key, tt.encode_text(text_tokens))
-        return self._txt_cache[1]
+                f = tt.encode_text(text_tokens)
+            self._txt_cache.put(text_tokens, key, f)
+        return f
 
     # ------------------------------------------------------------------ image side
     def _prompt_layers(self, g_prompt, e_prompt):

@@ -234,6 +234,14 @@ def counter_add(ctr, delta=1):
     call("lc_counter_add", stream_of(ctr), ctr.numel(), ptr(ctr), int(delta))
 
 
+def adam_step_advance(ctr, skip=None):
+    """ctr (int64 device scalar) += 1 unless skip[0] != 0: AdamW's step count advances only for
+    applied updates (GradScaler skips optimizer.step() on non-finite gradients)."""
+    if ctr.dtype != torch.int64 or ctr.numel() != 1:
+        raise ValueError("the AdamW step counter must be one int64 element")
+    call("lc_adam_step_advance", stream_of(ctr), ptr(ctr), ptr(skip))
+
+
 def l2norm_rows(f, out, norms):
     R, E = f.shape
     call("lc_l2norm_rows", stream_of(f), R, E, ptr(f), f.stride(0), ptr(out), ptr(norms))

@@ -18,6 +18,7 @@ from . import ops
 from .dp import DataParallel, layer_ranges
 from .adapter_clip import freeze_backbone
 from .ops import F32
+from .textcache import TokenFeatureCache
 
 
 class _nullctx:
@@ -77,12 +78,16 @@ class OnlineTrainer:
                 off += k
         self.params = params
         self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        # AdamW's step (bias correction) lives on the device and advances only for applied
+        # updates; step_count counts optimizer_step() calls, skipped ones included
+        self.adam_step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.step_count = 0
         self.graph = None
         self.overlap_text = bool(overlap_text)
         self.overlap_grads = bool(overlap_grads)
         self._side = None
         self._gstream = None
+        self._txt_cache = TokenFeatureCache()
         self.logit_scale = self.clip.logit_scale.detach().reshape(1)
 
     def reset_optimizer(self):
@@ -90,8 +95,7 @@ class OnlineTrainer:
         self.m.zero_()
         self.v.zero_()
         self.step_count = 0
-        if self.graph is not None:
-            self.ctr[1].zero_()
+        self.adam_step.zero_()
 
     def forward_backward(self, images, labels, tokens):
         """Everything but the optimizer update. Returns (loss[1], probs[B,C]).
@@ -107,6 +111,9 @@ class OnlineTrainer:
         side = self._side_stream(dev)
         if side is not None:
             side.wait_stream(main)
+        if not labels.is_cuda and labels.numel() and (int(labels.min()) < 0 or int(labels.max()) >= C):
+            raise ValueError(f"labels must index the {C} prompts (remap them against the global "
+                             "class list, trainer.remap_labels)")
         tok_in = dp.shard_tokens(tokens) if self.shard_text else tokens
         cached = self._cached_text(tokens)
         if cached is None:
@@ -162,25 +169,27 @@ class OnlineTrainer:
         dp.launch_bucket(self.flat_g, *self.txt_range)
         return loss, probs
 
-    # frozen text tower (peft_encoder 'image' / 'none'): its features depend only on the prompt
-    # tokens, so they are computed once per token tensor instead of every step
-    def _text_key(self, tokens):
-        if self.txt.stack.trainable_params() or torch.cuda.is_current_stream_capturing():
-            return None
+    # frozen text tower (peft_encoder 'image' / 'none'): features cached per token content
+    # (lcclip.textcache: rank-invariant hit decision, no stale hits on reused storage)
+    def _weights_key(self):
         c = self.clip
-        return (tokens.data_ptr(), tokens._version, tuple(tokens.shape),
-                tuple(p._version for p in c.transformer.parameters()),
+        return (tuple(p._version for p in c.transformer.parameters()),
                 c.token_embedding.weight._version, c.text_projection._version,
                 c.ln_final.weight._version)
 
+    def _cacheable(self):
+        return not (self.txt.stack.trainable_params() or torch.cuda.is_current_stream_capturing())
+
     def _cached_text(self, tokens):
-        key = self._text_key(tokens)
-        tc = getattr(self, "_txt_cache", None)
-        return tc[1] if (key is not None and tc is not None and tc[0] == key) else None
+        if not self._cacheable():
+            return None
+        return self._txt_cache.get(tokens, self._weights_key())
 
     def _store_text(self, tokens, f_t):
-        key = self._text_key(tokens)
-        self._txt_cache = (key, f_t) if key is not None else None
+        if self._cacheable():
+            self._txt_cache.put(tokens, self._weights_key(), f_t)
+        else:
+            self._txt_cache.clear()
 
     def _grad_stream(self, dev):
         if not self.overlap_grads:
@@ -217,11 +226,17 @@ class OnlineTrainer:
 
     def optimizer_step(self):
         self.step_count += 1
+        self._update()
+
+    def _update(self):
+        """Non-finite check -> AdamW step counter (unless skipped) -> fused AdamW, all on the
+        device (no host sync)."""
         self.skip.zero_()
         ops.check_finite(self.flat_g, self.skip)
+        ops.adam_step_advance(self.adam_step, self.skip)
         b1, b2 = self.betas
-        ops.adamw(self.flat_p, self.flat_g, self.m, self.v, self.lr, b1, b2, self.eps, self.wd,
-                  self.step_count, self.skip)
+        ops.adamw(self.flat_p, self.flat_g, self.m, self.v, self.lr, b1, b2, self.eps, self.wd, 1,
+                  self.skip, step_dev=self.adam_step)
         # the update bypassed torch's version counters: re-stage the PEFT-derived weights
         self.img.stack.invalidate_peft()
         self.txt.stack.invalidate_peft()
@@ -247,6 +262,7 @@ class OnlineTrainer:
         graph's input buffers (a later step() with other tensors copies into them). The dropout
         masks and AdamW's bias correction read device-side counters that the graph advances on
         every replay. Single process only: under torch.distributed the step stays eager.
+        step() then returns fresh copies of the graph's (loss, probs) buffers.
         Returns True when the graph is active."""
         if self.distributed:
             return False
@@ -254,19 +270,19 @@ class OnlineTrainer:
         self._gx = images
         self._gy = labels.to(dev, torch.int64).contiguous()
         self._gt = tokens.contiguous()
-        self.ctr = torch.zeros(2, dtype=torch.int64, device=dev)  # [rng epoch, adam step]
-        self.ctr[1] = self.step_count
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=dev)  # dropout RNG epoch
         for st in (self.img.stack, self.txt.stack):
             st.seed_dev = self.ctr[0:1]
         # warm-up steps (allocator, lazy staging) must not change the model: snapshot + restore
-        snap = [t.clone() for t in (self.flat_p, self.m, self.v, self.ctr)]
+        state = (self.flat_p, self.m, self.v, self.ctr, self.adam_step)
+        snap = [t.clone() for t in state]
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 self._graph_body()
         torch.cuda.current_stream(dev).wait_stream(side)
-        for t, c in zip((self.flat_p, self.m, self.v, self.ctr), snap):
+        for t, c in zip(state, snap):
             t.copy_(c)
         self.img.stack.invalidate_peft()
         self.txt.stack.invalidate_peft()
@@ -280,11 +296,7 @@ class OnlineTrainer:
     def _graph_body(self):
         ops.counter_add(self.ctr, 1)
         loss, probs = self.forward_backward(self._gx, self._gy, self._gt)
-        self.skip.zero_()
-        ops.check_finite(self.flat_g, self.skip)
-        b1, b2 = self.betas
-        ops.adamw(self.flat_p, self.flat_g, self.m, self.v, self.lr, b1, b2, self.eps, self.wd, 1,
-                  self.skip, step_dev=self.ctr[1:2])
+        self._update()
         # captured merges must re-run on every replay: stage again inside the next capture/run
         self.img.stack.invalidate_peft()
         self.txt.stack.invalidate_peft()
@@ -299,4 +311,5 @@ class OnlineTrainer:
             self._gt.copy_(tokens)
         self.graph.replay()
         self.step_count += 1
-        return self._g_out
+        # the captured outputs are overwritten by the next replay: hand out copies
+        return tuple(t.clone() for t in self._g_out)

@@ -103,3 +103,53 @@ def test_labels_tokenize_with_bpe():
     tok = m.labels_tokenize(["cat", "golden retriever"])
     assert tok.shape == (2, 77) and (tok[:, 0] == 49406).all()
     assert (tok.argmax(1) == torch.tensor([8, 9])).all()  # SOT + 6 template ids + name + '.'
+
+
+TOKEN_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                            "clip_tokens_cifar100.json")
+
+
+def _token_golden():
+    import json
+    with open(TOKEN_GOLDEN) as f:
+        return json.load(f)
+
+
+def test_token_fixture_known_ids():
+    """Runs without /root/reference: the committed CIFAR-100 prompt rows carry the public CLIP
+    ids of the template words ("a"=320, "bad"=2103, "photo"=1125, "of"=539, "."=269, SOT 49406,
+    EOT 49407), every row fits 77 tokens, and the class-name part differs between classes."""
+    d = _token_golden()
+    rows = d["ids"]
+    assert len(rows) == 100 and d["template"] == "a bad photo of a {}."
+    for name, ids in rows.items():
+        assert ids[:6] == [49406, 320, 2103, 1125, 539, 320], name
+        assert ids[-2:] == [269, 49407], name
+        assert len(ids) <= 77 and all(0 <= i < 49406 for i in ids[1:-1])
+    assert len({tuple(v[6:-2]) for v in rows.values()}) == 100
+
+
+def test_labels_tokenize_matches_fixture_rows():
+    """AdapterCLIP.labels_tokenize (models/adapter_clip.py:43-74: SOT + ids + EOT, zero padded to
+    77) over a tokenizer that replays the fixture's ids: the wrapper's row layout, no BPE file."""
+    from lcclip import AdapterCLIP
+    from tests.test_surface import TINY_ARCH
+    d = _token_golden()
+    table = {d["template"].format(n): ids[1:-1] for n, ids in d["ids"].items()}
+    m = AdapterCLIP("tiny", peft_method="adapter", peft_encoder="both", arch_overrides=TINY_ARCH,
+                    tokenizer=lambda text: table[text])
+    names = ["apple", "aquarium_fish", "wolf"]
+    tok = m.labels_tokenize(names)
+    assert tok.shape == (3, 77) and tok.dtype == torch.int64
+    for i, n in enumerate(names):
+        ids = d["ids"][n]
+        assert tok[i, :len(ids)].tolist() == ids and (tok[i, len(ids):] == 0).all()
+
+
+@pytest.mark.skipif(not os.path.isfile(BPE), reason="BPE merges file not available")
+def test_tokenizer_reproduces_token_fixture():
+    from lcclip.tokenizer import BPETokenizer
+    t = BPETokenizer(BPE)
+    d = _token_golden()
+    for name, ids in d["ids"].items():
+        assert [t.sot] + t.encode(d["template"].format(name)) + [t.eot] == ids, name

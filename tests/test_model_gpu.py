@@ -251,7 +251,7 @@ def test_graph_replay_matches_eager(golden, dev, method):
     r = ((tg.flat_p - te.flat_p).norm() / (te.flat_p - p0).norm()).item()
     record(test="graph_vs_eager", method=method, param_delta_rel=r)
     assert r < 1e-3
-    assert tg.ctr.tolist() == [3, 3]
+    assert tg.ctr.tolist() == [3] and tg.adam_step.tolist() == [3]
 
 
 def test_online_evaluate_and_frozen_text_cache(golden, dev):
@@ -279,7 +279,58 @@ def test_online_evaluate_and_frozen_text_cache(golden, dev):
     t2 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))
     l1, p1 = t1.forward_backward(img, y, tok)
     l1b, p1b = t1.forward_backward(img, y, tok)  # cache hit
-    t2._text_key = lambda tokens: None           # caching off
+    t2._cacheable = lambda: False                # caching off
     l2, p2 = t2.forward_backward(img, y, tok)
-    assert t1._txt_cache is not None
+    assert t1._txt_cache
     assert torch.equal(p1, p1b) and torch.equal(p1, p2) and torch.equal(l1, l2)
+
+
+def test_text_cache_freed_tokens_not_stale(golden, dev):
+    """a temporary token tensor freed after the step and a new one with other ids at
+    the same address / version must NOT hit the frozen-text cache."""
+    from lcclip import OnlineTrainer
+    d, _ = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    sdi = o.synthetic_state_dict(o.TINY, "adapter", "image", seed=3)
+    t1 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))
+    t2 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))
+    t2._cacheable = lambda: False
+    other = tok.clone()
+    other[:, 1] = (other[:, 1] + 17) % 49000 + 256  # different class names, same shape
+    t1.forward_backward(img, y, tok.clone())          # temporary: freed after the call
+    l1, p1 = t1.forward_backward(img, y, other.clone())
+    l2, p2 = t2.forward_backward(img, y, other)
+    assert torch.equal(p1, p2) and torch.equal(l1, l2)
+    # same content in a fresh tensor: a hit, same result
+    l3, p3 = t1.forward_backward(img, y, other.clone())
+    assert torch.equal(p3, p2)
+
+
+def test_adam_step_skipped_on_nonfinite(golden, dev):
+    """a skipped (non-finite) update leaves AdamW's step count alone, as the
+    reference's GradScaler skips optimizer.step()."""
+    from lcclip import OnlineTrainer
+    d, sd = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    ta = OnlineTrainer(make_wrapper(sd, "adapter", "both", dev), lr=5e-3)
+    tb = OnlineTrainer(make_wrapper(sd, "adapter", "both", dev), lr=5e-3)
+    ta.step(img, y, tok)
+    # b: one poisoned step first (label outside the class list -> NaN loss/gradients -> skip)
+    p0 = tb.flat_p.clone()
+    bad = y.clone()
+    bad[0] = tok.shape[0] + 5
+    lb, _ = tb.forward_backward(img, bad, tok)
+    tb.optimizer_step()
+    torch.cuda.synchronize()
+    assert not torch.isfinite(lb).all()
+    assert torch.equal(tb.flat_p, p0) and tb.adam_step.item() == 0
+    tb.step(img, y, tok)
+    torch.cuda.synchronize()
+    assert tb.adam_step.item() == 1
+    # the same first update as a trainer that never skipped (bias correction of step 1)
+    r = ((ta.flat_p - tb.flat_p).norm() / (ta.flat_p - p0).norm()).item()
+    assert r < 1e-3, r
