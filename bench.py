@@ -55,12 +55,12 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
 
 
 def routes_to_pp(M, N, K, epi):
-    """The lc_gemm_nt tile selector's rule for the 256x256 ping-pong kernel (gemm.hip,
-    lc_gemm_nt_ex): the dominant kernel of the step. The c_proj dX x QuickGELU' GEMM (EPI_MUL,
-    K <= 1024) goes to the 4-wave kernel instead."""
-    pp = N % 128 == 0 and M >= 4096 and N % 256 == 0 and (N >= 2048 or K >= 2048)
+    """The lc_gemm_nt tile selector's rule for the 256x256 phase-interleaved kernel (gemm.hip,
+    lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step. The c_proj dX x
+    QuickGELU' GEMM (EPI_MUL, K <= 1024, N >= 2048) goes to the 4-wave kernel instead."""
+    g8 = N % 128 == 0 and M >= 4096 and N % 256 == 0
     from lcclip.ops import EPI_MUL
-    return pp and not (epi == EPI_MUL and K <= 1024)
+    return g8 and not (epi == EPI_MUL and K <= 1024 and N >= 2048)
 
 
 class GemmTimer:
@@ -143,14 +143,14 @@ class TowerTimer:
 
 
 def pmc_traffic():
-    """HBM bytes per ping-pong launch from the latest committed PMC summary
+    """HBM bytes per launch of the dominant GEMM family from the latest committed PMC summary
     (tools/profile_round.sh + tools/pmc_traffic.py), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "gemm_traffic.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    fam = d.get("families", {}).get("gemm_pp_kernel")
+    fam = d.get("families", {}).get("gemm8_kernel_bf16")
     if not fam:
         return None, None
     return fam["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
@@ -334,8 +334,9 @@ def main():
                             "note": "SURVEY 8(d) north-star ratio: B*F_img / (t_image_tower * "
                                     "peak), HIP events around the tower's fwd and bwd"},
             "roofline": {"bound": "mfma",
-                         "kernel": "gemm_pp_kernel<EPI 0|6> (256x256 ping-pong bf16 MFMA GEMM: "
-                                   "QKV, c_fc+QuickGELU+QuickGELU', c_proj fwd; QKV, c_fc dX)",
+                         "kernel": "gemm8_kernel<EPI 0|2|6, bf16> (256x256 phase-interleaved "
+                                   "bf16 MFMA GEMM: QKV, out-proj, c_fc+QuickGELU+QuickGELU', "
+                                   "c_proj fwd; QKV, out-proj, c_fc dX)",
                          "achieved": round(achieved / 1e12, 2), "peak": PEAK_BF16 / 1e12,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4),
                          "traffic": None if traffic is None else round(traffic),

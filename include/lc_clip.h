@@ -62,9 +62,33 @@ int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* 
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes);
 
+/* Block-scaled fp8 GEMM (MX-style e4m3 operands, E8M0 scale per 32 k; fp8 MFMA
+ * v_mfma_scale_f32_16x16x128_f8f6f4 at twice the bf16 rate): out = epilogue(alpha * A @ B^T + bias)
+ * with A [M,K] / B [N,K] e4m3 (row strides lda / ldb in BYTES, multiples of 16) and their scales
+ * sa [K/128][sa_rows][4] / sb [K/128][sb_rows][4] (sa_rows = M rounded up to 256, sb_rows >= N;
+ * lc_quant_fp8 produces both). K % 128 == 0, N % 256 == 0. Epilogues LC_EPI_BF16 / F32 / RESID /
+ * GELU / GELU_D / MUL as lc_gemm_nt; ws as lc_gemm_nt_ws.
+ * Replaces: the fp16 frozen-backbone GEMMs of MaPLe (models/maple_clip/model.py:749-772, 826:
+ * convert_weights to half; the QKV / c_fc / c_proj products of :316-401), run in fp8 as BASELINE
+ * config 5 names. */
+int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                   const void* sa, long sa_rows, const void* B, long ldb, const void* sb,
+                   long sb_rows, const float* bias, float alpha, void* out0, long ldo0,
+                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes);
+
+/* Quantise src [rows, K] (bf16, or f32 when src_f32; element (r, k) at src[r*sr + k*sk], so a
+ * transposed view quantises along its other axis) to e4m3 dst [rows, ldd] + E8M0 scales
+ * [K/128][rows_pad][4]: per block of 32 k, scale = 2^(floor(log2 amax) - 8) clamped to
+ * [2^-126, 2^126] (amax = 0 -> scale byte 0, values 0), value = RNE_e4m3(clamp(x / scale, +-448)).
+ * K % 128 == 0, rows_pad % 256 == 0. */
+int lc_quant_fp8(hipStream_t stream, long rows, int K, const void* src, int src_f32, long sr,
+                 long sk, void* dst, long ldd, void* scales, long rows_pad);
+
 /* Tile-shape override for lc_gemm_nt (tuning): 0 = automatic, 1 = 128x128 (4 waves),
  * 2 = 256x128 (8 waves, 3-stage LDS ring), 3 = 256x256 (8 waves, 2 stages), 4 = 128x64,
- * 5 = 256x256 ping-pong (8 waves in two staggered groups, 4-slot k-half LDS ring), 6 = same.
+ * 5 = 256x256 ping-pong (8 waves in two staggered groups, 4-slot k-half LDS ring), 6 = same,
+ * 7 = 256x256 4-wave AGPR kernel, 8 = 256x256 phase-interleaved kernel (the fp8 GEMM's, bf16),
+ * 11 = 128x64 one-stage.
  * The environment variable LC_GEMM_TILE sets the initial value. */
 int lc_gemm_set_tile(int tile);
 

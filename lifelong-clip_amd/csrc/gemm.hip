@@ -573,6 +573,294 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Phase-interleaved GEMM, bf16 or block-scaled fp8 (256 x 256 tile, 512 threads).
+// 8 waves = 2 groups (wr = wave / 4: A rows 128 wr .. +127) x 4 (wc: B rows 64 wc .. +63); each
+// wave owns a 128 x 64 output = 8 x 4 subtiles of 16 x 16 (128 accumulator VGPRs). K goes in
+// k-tiles of 128 B per row (64 bf16 or 128 e4m3), double-buffered in LDS: A [256][128 B] + B
+// [256][128 B] (+ 2 KiB of E8M0 scales for fp8) per buffer = 129 / 131 KiB in total.
+// A k-tile is 4 phases, one per quadrant (qm, qn) of the wave's output, in the order (0,0),
+// (0,1), (1,0), (1,1): LOAD part (this quadrant's fragments not yet in registers — A(qm0) + B(qn0)
+// = 12 ds_read_b128, B(qn1) = 4, A(qm1) = 8, then none — plus one quarter of the DMA of a later
+// k-tile), barrier, MFMA part (16 bf16 16x16x32 or 8 scaled 16x16x128 MFMAs = 256 cycles),
+// barrier. Group 1 runs one barrier behind group 0, so on every SIMD one wave's MFMA part
+// overlaps the other's LOAD part.
+// DMA quarters (16 KiB, 2 global_load_lds per thread) in issue order: phase 0 of k-tile t: B rows
+// 128..255 of t+1; phase 1: A rows 0..127 of t+1 (+ the scale piece of t+1); phase 2: A rows
+// 128..255 of t+1; phase 3: B rows 0..127 of t+2. Hazards (barriers numbered by interval; G0's
+// LOAD(P) is interval 2P, G1's 2P+1): WAR — the first DMA into a buffer (B-lo of t+2, phase 3 of
+// t) follows the last read of B(t) (G1's phase-1 LOAD, retired in its phase-1 MFMA) by one
+// interval, A-top(t+2) / A-bot(t+2) follow the last A reads of t by >= 5. RAW — before G0 reads
+// k-tile t+1 (phase 0: A-top, B, scales) every wave has retired B-lo, B-hi, A-top(t+1): G0 at the
+// end of its phase-3 MFMA, G1 at the end of its phase-3 LOAD (each leaves A-bot(t+1) and
+// B-lo(t+2) in flight: vmcnt(4)); before G1 reads it (A-bot too) G0 retires A-bot(t+1) at the
+// end of its next LOAD (B-lo, B-hi of t+2 in flight) and G1 at the end of its phase-3 MFMA
+// (B-lo(t+2) in flight).
+// A lane (g = lane >> 4) reads 16-B chunks g and g + 4 of a 128-B row in both forms: the bf16
+// operand's k-steps 0 and 1, and for fp8 exactly the bytes v_mfma_scale_f32_16x16x128_f8f6f4
+// takes from lane group g (k 16g..16g+15 in bytes 0-15, 64+16g.. in bytes 16-31; measured with
+// tools/dbg_fp8.py: hardware scale block b = k / 32 takes lane group b's scale byte, so each
+// lane passes the scale of block g). Conflict-free under the row XOR swizzle chunk ^ ((row >> 1) & 7).
+template <int EPI, bool FP8>
+__global__ void __launch_bounds__(512, 1)
+gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
+             const void* __restrict__ Bv, long ldb, const float* __restrict__ bias, float alpha,
+             void* __restrict__ out0, long ldo0, void* __restrict__ out1, long ldo1,
+             const void* __restrict__ aux, long ldaux, EpiParams ep, SplitK sk, Fp8Scales sc) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 8 x 4 subtiles per wave
+  constexpr int TILE_A = BM * 128, TILE_B = BN * 128;
+  constexpr int SCALES = FP8 ? 2048 : 0;
+  constexpr int BUF = TILE_A + TILE_B + SCALES;
+  constexpr int SWM = 7;
+  constexpr int KT = FP8 ? 128 : 64;  // k per k-tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int tiles_n = N / BN;
+  int bid = blockIdx.x;
+  int split = -1;
+  int tb = 0, te = K / KT;  // k-tiles [tb, te) of this workgroup
+  if (bid < sk.dp_tiles) {
+    const int nwg = sk.dp_tiles;
+    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+  } else {
+    const int s_id = bid - sk.dp_tiles;
+    split = s_id % sk.splits;
+    bid = sk.dp_tiles + s_id / sk.splits;
+    const int nt_all = K / KT;
+    tb = split * nt_all / sk.splits;
+    te = (split + 1) * nt_all / sk.splits;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nt = te - tb;
+  const char* __restrict__ A = static_cast<const char*>(Av) + (long)tb * 128;
+  const char* __restrict__ B = static_cast<const char*>(Bv) + (long)tb * 128;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DMA quarter `kind` of k-tile t: 0 = B rows 0..127, 1 = B rows 128..255, 2 = A rows 0..127
+  // (+ scales), 3 = A rows 128..255
+  auto dma = [&](int t, int kind) {
+    char* buf = smem + (t & 1) * BUF;
+    const bool isA = kind >= 2;
+    const int half = kind & 1;
+    const char* g = isA ? A : B;
+    const long ld = isA ? lda : ldb;
+    const int rows_valid = isA ? M : N;
+    const int r0 = isA ? m0 : n0;
+    char* dst = buf + (isA ? 0 : TILE_A) + half * (128 * 128);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = half * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & SWM);
+      int gr = r0 + row;
+      gr = gr < rows_valid ? gr : rows_valid - 1;  // tail rows computed, never stored
+      glds16(g + (long)gr * ld + (long)t * 128 + c * 16, dst + (wave * 2 + i) * 1024);
+    }
+    if constexpr (FP8) {
+      if (kind == 2) {
+        // 2 KiB of scales: waves 0-3 -> A rows 64 w .. +63, waves 4-7 -> B rows
+        const bool sA = wave < 4;
+        const long rows_pad = sA ? sc.sa_rows : sc.sb_rows;
+        const uint8_t* s = sA ? sc.sa : sc.sb;
+        const int row = (wave & 3) * 64 + lane;
+        glds4(s + ((long)(tb + t) * rows_pad + (sA ? m0 : n0) + row) * 4,
+              buf + TILE_A + TILE_B + (sA ? 0 : 1024) + (wave & 3) * 256);
+      }
+    }
+  };
+
+  const int g = lane >> 4, t16 = lane & 15;
+  using Frag = typename std::conditional<FP8, i32x8, bf16x8[2]>::type;
+  Frag fa[4], fb[2][2];
+  uint32_t sfa[4], sfb[2][2];
+  (void)sfa;
+  (void)sfb;
+  // Lane-constant parts of the fragment addresses: the swizzle term (row >> 1) & SWM only
+  // depends on t16 (subtile rows start at multiples of 16), so every read is a per-lane base plus
+  // an immediate. Chunks g and g + 4: c1 = c0 ^ 64.
+  const int sw = (t16 >> 1) & SWM;
+  const int c0 = (g ^ sw) << 4;
+  const int c1 = c0 ^ 64;
+  const int a_row = (wr * 128 + t16) * 128, b_row = TILE_A + (wc * 64 + t16) * 128;
+  auto read_frag = [&](const char* p0, const char* p1, auto& f) {
+    if constexpr (FP8) {
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(p0);
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(p1);
+      f = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    } else {
+      f[0] = *reinterpret_cast<const bf16x8*>(p0);
+      f[1] = *reinterpret_cast<const bf16x8*>(p1);
+    }
+  };
+  // scale byte of (row, this lane's k-block g): byte g of the row's k-tile dword
+  auto read_scale = [&](const char* p) -> uint32_t {
+    return *reinterpret_cast<const uint8_t*>(p + g);
+  };
+  auto load_a = [&](const char* buf, int qm) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ro = (qm * 64 + i * 16) * 128;
+      read_frag(buf + a_row + ro + c0, buf + a_row + ro + c1, fa[i]);
+      if constexpr (FP8)
+        sfa[i] = read_scale(buf + TILE_A + TILE_B + (wr * 128 + t16 + qm * 64 + i * 16) * 4);
+    }
+  };
+  auto load_b = [&](const char* buf, int qn) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ro = (qn * 32 + j * 16) * 128;
+      read_frag(buf + b_row + ro + c0, buf + b_row + ro + c1, fb[qn][j]);
+      if constexpr (FP8)
+        sfb[qn][j] = read_scale(buf + TILE_A + TILE_B + 1024 + (wc * 64 + t16 + qn * 32 + j * 16) * 4);
+    }
+  };
+  // The MFMA cluster is pinned between its barriers: the empty asm statements redefine the
+  // quadrant's accumulators before the cluster and consume them after it, and volatile asm stays
+  // in order with s_barrier. (hipcc otherwise sinks the register-only scaled MFMAs into the
+  // loop latch: all fragments of a k-tile stay live and spill.)
+  auto pin = [&](int qm, int qn) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[qm * 4 + i][qn * 2 + j]));
+  };
+  auto mma = [&](int qm, int qn) {
+    pin(qm, qn);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4& c = acc[qm * 4 + i][qn * 2 + j];
+        if constexpr (FP8) {
+          c = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[qn][j], fa[i], c, 0, 0, 0,
+                                                               sfb[qn][j], 0, sfa[i]);
+        } else {
+          c = mfma16(fb[qn][j][0], fa[i][0], c);
+          c = mfma16(fb[qn][j][1], fa[i][1], c);
+        }
+      }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pin(qm, qn);
+  };
+  const bool g0 = wr == 0;
+
+  // prologue: k-tile 0 whole, B rows 0..127 of k-tile 1; everything landed
+  dma(0, 0);
+  dma(0, 1);
+  dma(0, 2);
+  dma(0, 3);
+  if (nt > 1) dma(1, 0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (!g0) __builtin_amdgcn_s_barrier();  // group 1 one barrier behind
+
+  for (int t = 0; t < nt; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+    // ---- phase 0: quadrant (0,0)
+    load_a(buf, 0);
+    load_b(buf, 0);
+    if (n1) dma(t + 1, 1);
+    if (g0) {  // A rows 128..255 of k-tile t retired (group 1 reads them next interval)
+      if (n1) wait_vmcnt<4>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    mma(0, 0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 1: quadrant (0,1)
+    load_b(buf, 1);
+    if (n1) dma(t + 1, 2);
+    __builtin_amdgcn_s_barrier();
+    mma(0, 1);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: quadrant (1,0)
+    load_a(buf, 1);
+    if (n1) dma(t + 1, 3);
+    __builtin_amdgcn_s_barrier();
+    mma(1, 0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 3: quadrant (1,1), no reads
+    if (n2) dma(t + 2, 0);
+    if (!g0) {  // B and A rows 0..127 (+ scales) of k-tile t+1 retired
+      if (n2) wait_vmcnt<4>();
+      else if (n1) wait_vmcnt<2>();
+    }
+    __builtin_amdgcn_s_barrier();
+    mma(1, 1);
+    if (g0) {
+      if (n2) wait_vmcnt<4>();
+      else if (n1) wait_vmcnt<2>();
+    } else {  // A rows 128..255 of k-tile t+1 retired
+      if (n2) wait_vmcnt<2>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+  if (g0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if (split >= 0) {
+    const int tail = bid - sk.dp_tiles;
+    constexpr int SLAB = BM * BN;
+    float* mine = sk.slabs + ((long)tail * sk.splits + split) * SLAB;
+    const int lane_off = (wave * TM * TN * 64 + lane) * 4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(mine + lane_off + (i * TN + j) * 256) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int ticket = __hip_atomic_fetch_add(sk.tickets + tail, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const int last = ticket == sk.splits - 1;
+      if (last) {
+        __hip_atomic_store(sk.tickets + tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();
+    if (!last) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < sk.splits; ++s) {
+      const float* other = sk.slabs + ((long)tail * sk.splits + s) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += *reinterpret_cast<const f32x4*>(other + lane_off + (i * TN + j) * 256);
+    }
+  } else {
+    __builtin_amdgcn_s_barrier();  // every wave done with the ring: the epilogue reuses it
+  }
+  store_tile<BM, BN, WM, WN, EPI>(acc, smem, 2 * BUF, m0, n0, M, bias, alpha, out0, ldo0, out1,
+                                  ldo1, aux, ldaux, ep);
+}
+
+// ---------------------------------------------------------------------------------------------
 // 4-wave 256x256 GEMM (one wave per SIMD, each wave a 128x128 sub-tile: 64 accumulator tiles in
 // AGPRs). K is consumed in 32-deep steps through a 4-slot LDS ring (slot = A [256][32] + B
 // [256][32] bf16 in 64-B rows, the ping-pong kernel's layout and swizzle); the DMA of step s+3 is
@@ -1129,9 +1417,10 @@ int cu_count() {
   return cus[dev];
 }
 
-// Split-K plan for the tail round (see SplitK): S slices of >= 16 k-halves each, R*S <= CUs,
-// only when the last round is at most half full and the workspace holds the slabs.
-SplitK plan_split(int tiles, int K, void* ws, long ws_bytes) {
+// Split-K plan for the tail round (see SplitK): S slices of >= min_units k-units each (units =
+// the kernel's k-steps), R*S <= CUs, only when the last round is at most half full and the
+// workspace holds the slabs.
+SplitK plan_split(int tiles, int units, int min_units, void* ws, long ws_bytes) {
   SplitK sk{tiles, 1, nullptr, nullptr};
   if (g_split_mode < 0) {
     const char* e = getenv("LC_GEMM_SPLITK");
@@ -1143,8 +1432,7 @@ SplitK plan_split(int tiles, int K, void* ws, long ws_bytes) {
   if (tiles < cus || rem == 0 || rem > cus / 2) return sk;
   int S = cus / rem;
   S = S > 4 ? 4 : S;
-  const int nh = K / 32;
-  if (S > nh / 16) S = nh / 16;  // measured: slices under 16 halves (K = 768) lose
+  if (S > units / min_units) S = units / min_units;  // measured: slices under 16 halves (K = 768) lose
   if (S < 2) return sk;
   const long tick_bytes = LC_SPLITK_TICKET_BYTES;
   if ((long)rem * 4 > tick_bytes || tick_bytes + (long)rem * S * 256 * 256 * 4 > ws_bytes) return sk;
@@ -1183,7 +1471,7 @@ int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
               void* o1, long l1, const void* aux, long la, const EpiParams& ep, void* ws,
               long ws_bytes) {
   const int tiles = ((M + 255) / 256) * (N / 256);
-  const SplitK sk = plan_split(tiles, K, ws, ws_bytes);
+  const SplitK sk = plan_split(tiles, K / 32, 16, ws, ws_bytes);
   dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
 #define LC_PP_CASE(E)                                                                          \
   case E:                                                                                      \
@@ -1207,6 +1495,37 @@ int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
       return LC_EINVAL;
   }
 #undef LC_PP_CASE
+  LC_LAUNCH_RET();
+}
+
+// Phase-interleaved 256x256 GEMM (gemm8_kernel). bf16: A, B bf16 with lda/ldb in elements;
+// fp8: A, B e4m3 with lda/ldb in bytes and their E8M0 scales in sc.
+template <bool FP8>
+int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long lda,
+              const void* B, long ldb, const float* bias, float alpha, void* o0, long l0,
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep, void* ws,
+              long ws_bytes, const Fp8Scales& sc) {
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  const int units = K / (FP8 ? 128 : 64);
+  const SplitK sk = plan_split(tiles, units, 8, ws, ws_bytes);
+  const long ea = FP8 ? 1 : 2;  // bytes per element
+  dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
+#define LC_G8_CASE(E)                                                                          \
+  case E:                                                                                      \
+    hipLaunchKernelGGL((gemm8_kernel<E, FP8>), grid, block, 0, st, M, N, K, A, lda * ea, B,    \
+                       ldb * ea, bias, alpha, o0, l0, o1, l1, aux, la, ep, sk, sc);            \
+    break;
+  switch (epi) {
+    LC_G8_CASE(EPI_BF16)
+    LC_G8_CASE(EPI_F32)
+    LC_G8_CASE(EPI_RESID)
+    LC_G8_CASE(EPI_GELU)
+    LC_G8_CASE(EPI_GELU_D)
+    LC_G8_CASE(EPI_MUL)
+    default:
+      return LC_EINVAL;
+  }
+#undef LC_G8_CASE
   LC_LAUNCH_RET();
 }
 
@@ -1243,19 +1562,21 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   }
   int tile = g_force_tile;
   if (tile == 0) {
-    // measured on the ViT-B/16 step shapes (tools/bench_gemm.py): 256x256 ping-pong for the
-    // wide (N >= 2048) and deep (K >= 2048) GEMMs, 128x128 at 2 workgroups/CU otherwise
+    // measured on the ViT-B/16 step shapes (tools/bench_gemm.py, M = 50 432): the 256x256
+    // phase-interleaved kernel beats the ping-pong one on every shape (776-1113 vs 743-1044 TF)
+    // and the 128x128 kernel on N = K = 768 (858 vs ~780 TF); 128x128 at 2 workgroups/CU for
+    // the small-M (text tower) launches
     if (N % 128 != 0) tile = 4;
-    else if (M >= 4096 && N % 256 == 0 && (N >= 2048 || K >= 2048)) tile = 5;
+    else if (M >= 4096 && N % 256 == 0) tile = 8;
     else tile = 1;
-    // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 298 vs 315 us (bench_gemm.py)
-    if (tile == 5 && epi == EPI_MUL && K <= 1024) tile = 7;
+    // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 289 vs 295 us (bench_gemm.py)
+    if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048) tile = 7;
     // one-k-tile streams (adapter up-projection / input gradient, K = 64): 128x64 tiles keep
     // more rows in flight per CU (tools/bench_adapter_kernels.py: AD_UP 83 -> 77 us, AD_ADD
     // 37 -> 35 us)
     if (K <= 64) tile = 11;
   }
-  if (((tile == 3 || tile == 5 || tile == 6 || tile == 7) && N % 256) ||
+  if (((tile == 3 || tile == 5 || tile == 6 || tile == 7 || tile == 8) && N % 256) ||
       ((tile == 1 || tile == 2) && N % 128))
     tile = 4;
   switch (tile) {
@@ -1275,6 +1596,13 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     case 6:
       return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                        aux, ldaux, ep, ws, ws_bytes);
+    case 8:
+      if (epi != EPI_BF16 && epi != EPI_F32 && epi != EPI_RESID && epi != EPI_GELU &&
+          epi != EPI_GELU_D && epi != EPI_MUL)
+        return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                         aux, ldaux, ep, ws, ws_bytes);
+      return launch_g8<false>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1,
+                              ldo1, aux, ldaux, ep, ws, ws_bytes, Fp8Scales{});
     case 11:  // 128x64, one LDS stage
       return launch_nt<128, 64, 4, 1, 1>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                          ldo0, out1, ldo1, aux, ldaux, ep);
@@ -1307,6 +1635,27 @@ int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* 
 int lc_gemm_set_debug(unsigned long long* p) {
   g_dbg = p;
   return LC_OK;
+}
+
+int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                   const void* sa, long sa_rows, const void* B, long ldb, const void* sb,
+                   long sb_rows, const float* bias, float alpha, void* out0, long ldo0,
+                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes) {
+  LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 256 == 0);
+  LC_CHECK_ARG(lda % 16 == 0 && ldb % 16 == 0 && lda >= K && ldb >= K);
+  LC_CHECK_ARG(sa != nullptr && sb != nullptr && sa_rows >= (M + 255) / 256 * 256 &&
+               sb_rows >= N && sa_rows % 256 == 0 && sb_rows % 256 == 0);
+  LC_CHECK_ARG(((uintptr_t)sa & 15) == 0 && ((uintptr_t)sb & 15) == 0);
+  LC_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_RESID || epi == EPI_GELU ||
+               epi == EPI_GELU_D || epi == EPI_MUL);
+  LC_CHECK_ARG(ldo0 % 8 == 0 && ldo0 >= N);
+  if (epi == EPI_GELU || epi == EPI_GELU_D) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
+  if (epi == EPI_RESID || epi == EPI_MUL) LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
+  LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
+  EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
+  Fp8Scales sc{static_cast<const uint8_t*>(sa), static_cast<const uint8_t*>(sb), sa_rows, sb_rows};
+  return launch_g8<true>(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
+                         aux, ldaux, ep, ws, ws_bytes, sc);
 }
 
 int lc_gemm_set_tile(int tile) {

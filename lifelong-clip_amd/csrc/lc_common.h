@@ -9,10 +9,21 @@ typedef uint16_t bf16_t;  // raw bf16 bits in global memory
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));  // 32 fp8 e4m3 (one 16x16x128 operand)
 
 #define LC_DEV __device__ __forceinline__
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 #define GLB_PTR(p) ((const __attribute__((address_space(1))) void*)(p))
+
+// Block-scaled fp8 operand format of the fp8 GEMMs (MX-style, OCP e4m3fn elements): a [rows, K]
+// row-major e4m3 matrix plus one E8M0 scale byte per 32 consecutive k of a row (value =
+// e4m3 * 2^(byte - 127)). The scale bytes are stored k-tile-major, [K/128][rows_pad][4]: the
+// 4 bytes of (k-tile, row) are the 4 blocks of that row's 128 k — one 1-KiB contiguous piece per
+// 256-row tile and k-tile. rows_pad = rows rounded up to 256 (tile loads never leave the buffer).
+LC_DEV long fp8_scale_index(long row, int kblock, long rows_pad) {
+  return ((long)(kblock >> 2) * rows_pad + row) * 4 + (kblock & 3);
+}
 
 LC_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 LC_DEV float bf2f_s(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
@@ -37,6 +48,10 @@ LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 // Async 16-byte global -> LDS copy; LDS destination = wave-uniform base + lane * 16.
 LC_DEV void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+// 4-byte form: LDS destination = wave-uniform base + lane * 4.
+LC_DEV void glds4(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 4, 0, 0);
 }
 
 LC_DEV float wave_sum(float v) {
@@ -92,7 +107,40 @@ struct EpiParams {
   uint64_t seed;     // dropout mask seed
   unsigned long long* dbg;  // diagnostic timestamps (nullptr in production)
   const unsigned long long* seed_dev;  // optional device-side RNG epoch added to seed (graphs)
+  uint8_t* q_scale;  // fp8-output epilogues: E8M0 scales of the fp8 output ([N/128][q_rows][4])
+  long q_rows;       // padded row count of that scale buffer
 };
+
+// fp8 operand scales of a block-scaled GEMM (see fp8_scale_index)
+struct Fp8Scales {
+  const uint8_t* sa;  // A's scales, rows_pad = sa_rows
+  const uint8_t* sb;  // B's scales
+  long sa_rows, sb_rows;
+};
+
+// E8M0 block scale of a 32-element block with max |x| = amax (OCP MX: 2^(floor(log2 amax) - 8),
+// e4m3's largest power being 2^8), clamped to [2^-126, 2^126]; amax = 0 (or below the f32 normal
+// range) -> byte 0, every element encodes to 0.
+LC_DEV uint32_t e8m0_of(float amax) {
+  const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);
+  if (e == 0) return 0;
+  const int b = e - 8;
+  return (uint32_t)(b < 1 ? 1 : (b > 253 ? 253 : b));
+}
+// 2^-(byte - 127) as f32 (the multiplier that maps a block into e4m3 range); byte 0 -> 0
+LC_DEV float e8m0_inv(uint32_t byte) {
+  if (byte == 0) return 0.f;
+  return __uint_as_float((uint32_t)(254 - byte) << 23);
+}
+// four f32 -> four e4m3fn bytes (RNE), saturated to +-448 first
+LC_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  uint32_t r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+}
 
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).
 int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,

@@ -58,6 +58,75 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
     return out0
 
 
+# ------------------------------------------------------------------ block-scaled fp8 operands
+FP8 = torch.uint8  # e4m3fn codes are carried as raw bytes
+
+
+class Fp8Mat:
+    """A [rows, K] e4m3 matrix in the fp8 GEMMs' operand format (lc_common.h): `data` uint8
+    [rows, K] codes, `scales` uint8 [K/128, rows_pad, 4] E8M0 bytes (rows_pad = rows rounded up to
+    256)."""
+    __slots__ = ("data", "scales", "rows", "K")
+
+    def __init__(self, rows, K, device, data=None, scales=None):
+        if K % 128:
+            raise ValueError("fp8 operands need K % 128 == 0")
+        pad = (rows + 255) // 256 * 256
+        self.rows, self.K = rows, K
+        self.data = data if data is not None else torch.empty((rows, K), dtype=FP8, device=device)
+        self.scales = scales if scales is not None else torch.zeros((K // 128, pad, 4), dtype=FP8,
+                                                                  device=device)
+
+    @property
+    def rows_pad(self):
+        return self.scales.shape[1]
+
+    def narrow(self, rows):
+        """The first `rows` rows (a view; the scale buffer keeps its padded row count)."""
+        out = Fp8Mat.__new__(Fp8Mat)
+        out.data, out.scales, out.rows, out.K = self.data[:rows], self.scales, rows, self.K
+        return out
+
+
+def quant_fp8(src, out=None, transpose=False):
+    """src [rows, K] bf16 or f32 (transpose=True: quantise src^T, i.e. along src's rows) ->
+    Fp8Mat. Weights are quantised straight from their f32 master copy."""
+    if src.dtype not in (BF16, F32) or src.dim() != 2:
+        raise TypeError("quant_fp8: src must be a 2-D bf16 or f32 tensor")
+    if transpose:
+        K, rows = src.shape
+        sr, sk = src.stride(1), src.stride(0)
+    else:
+        rows, K = src.shape
+        sr, sk = src.stride(0), src.stride(1)
+    if out is None:
+        out = Fp8Mat(rows, K, src.device)
+    if out.rows != rows or out.K != K:
+        raise ValueError("quant_fp8: output shape mismatch")
+    call("lc_quant_fp8", stream_of(src), rows, K, ptr(src), 1 if src.dtype == F32 else 0, sr, sk,
+         ptr(out.data), out.data.stride(0), ptr(out.scales), out.rows_pad)
+    return out
+
+
+def gemm_nt_fp8(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
+    """out = epilogue(alpha * A @ B^T + bias) with A, B Fp8Mat (block-scaled e4m3) on the fp8
+    MFMA; epilogues as gemm_nt (BF16, F32, RESID, GELU, GELU_D, MUL)."""
+    M, K = A.rows, A.K
+    N = B.rows
+    if B.K != K or out0.shape[0] != M or out0.shape[1] != N:
+        raise ValueError(f"gemm_nt_fp8 shapes A[{M},{K}] B[{N},{B.K}] out{tuple(out0.shape)}")
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("gemm_nt_fp8 bias must be a contiguous f32 vector of length N")
+    st = stream_of(A.data)
+    ws = splitk_workspace(torch.cuda.current_stream(A.data.device))
+    call("lc_gemm_nt_fp8", st, epi, M, N, K, ptr(A.data), A.data.stride(0), ptr(A.scales),
+         A.rows_pad, ptr(B.data), B.data.stride(0), ptr(B.scales), B.rows_pad, ptr(bias),
+         float(alpha), ptr(out0), out0.stride(0), ptr(out1),
+         out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
+         ptr(ws), ws.numel())
+    return out0
+
+
 def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
     """C[N1,N2] += alpha * A[M,:N1]^T @ B[M,:N2] (C f32, N1 x N2 = C's shape); colsum[N1] +=
     colsum_scale * sum_m A[:, :N1]. A / B may be wider than N1 / N2 (zero padding to 64)."""

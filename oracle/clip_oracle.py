@@ -181,10 +181,79 @@ def quick_gelu(x):
     return x * torch.sigmoid(1.702 * x)
 
 
-def linear(x, w, b=None, rt=identity):
-    """F.linear with operands rounded at the GEMM input (fp32 accumulate)."""
-    y = rt(x) @ rt(w).t()
+def linear(x, w, b=None, rt=identity, fp8=False):
+    """F.linear with operands rounded at the GEMM input (fp32 accumulate). fp8=True marks the
+    frozen-backbone GEMMs (QKV, c_fc, c_proj) that an fp8 rounding hook (``fp8_rounding``)
+    evaluates as block-scaled e4m3 GEMMs, forward and input-gradient (``Fp8Linear``)."""
+    if fp8 and getattr(rt, "fp8", False):
+        y = Fp8Linear.apply(x, w)
+    else:
+        y = rt(x) @ rt(w).t()
     return y if b is None else y + b
+
+
+# ----------------------------------------------------------------------------- fp8 rounding
+# The block-scaled fp8 operand format of the MI355X fp8 GEMMs (BASELINE config 5 runs MaPLe's
+# frozen backbone in fp8; the reference's own MaPLe casts it to fp16, models/maple_clip/
+# model.py:749-772, 826). Restated from the OCP Microscaling (MX) v1.0 definition: blocks of 32
+# consecutive elements along the reduction axis share an E8M0 scale X = 2^(floor(log2 amax) -
+# emax_elem) with emax_elem = 8 for e4m3 (largest normal 448 = 1.75 * 2^8); each element is
+# RNE(x / X) in OCP e4m3fn, saturated to +-448 (the conversion torch.float8_e4m3fn implements).
+# Build choices beyond the spec, mirrored by the kernels: the scale exponent is clamped to
+# [-126, 126]; a block whose amax is 0 or below the f32 normal range gets scale byte 0 and
+# zero values.
+def fp8_scale_bytes(amax):
+    """E8M0 byte of each block's scale from its amax (f32 tensor)."""
+    e = (amax.float().contiguous().view(torch.int32) >> 23) & 0xFF
+    b = (e - 8).clamp(1, 253)
+    return torch.where(e == 0, torch.zeros_like(b), b)
+
+
+def quant_fp8(x):
+    """x [..., K] (K % 32 == 0) -> (codes uint8 [..., K], scale bytes uint8 [..., K/32],
+    dequantised f32 [..., K])."""
+    *lead, K = x.shape
+    xb = x.detach().float().reshape(*lead, K // 32, 32)
+    byte = fp8_scale_bytes(xb.abs().amax(-1))
+    inv = torch.where(byte == 0, torch.zeros_like(byte, dtype=torch.float32),
+                      torch.exp2((127 - byte).float()))
+    q = (xb * inv[..., None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+    deq = q.float() * torch.exp2((byte - 127).float())[..., None]
+    deq = torch.where(byte[..., None] == 0, torch.zeros_like(deq), deq)
+    return (q.view(torch.uint8).reshape(*lead, K), byte.to(torch.uint8),
+            deq.reshape(*lead, K))
+
+
+def fp8_round(x):
+    """Value of x after the fp8 round trip along its last axis (no gradient path)."""
+    return quant_fp8(x)[2]
+
+
+class Fp8Linear(torch.autograd.Function):
+    """y = fp8(x) @ fp8(W)^T with both operands quantised along K (the forward fp8 GEMM);
+    dx = fp8(dy) @ fp8(W^T)^T with dy and W^T quantised along N (the input-gradient fp8 GEMM, W
+    transposed and quantised once per checkpoint). W is frozen: no weight gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(w)
+        return fp8_round(x) @ fp8_round(w).t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        (w,) = ctx.saved_tensors
+        return fp8_round(dy) @ fp8_round(w.t().contiguous()).t(), None
+
+
+def fp8_rounding(base=None):
+    """A rounding hook for the oracle's ``rt`` argument: ``base`` (default round_bf16) everywhere,
+    plus block-scaled fp8 GEMMs where ``linear(..., fp8=True)``."""
+    base = round_bf16 if base is None else base
+
+    def rt(x):
+        return base(x)
+    rt.fp8 = True
+    return rt
 
 
 def merged_lora_weight(w, a, bmat, scaling, rt=identity):
@@ -228,7 +297,7 @@ def mha(x, p, pre, n_head, causal, lora_scaling=None, rt=identity):
                                   p[pre + "attn.in_proj_weight_lora_B"], lora_scaling, rt)
         w_out = merged_lora_weight(w_out, p[pre + "attn.out_proj.lora_A"],
                                    p[pre + "attn.out_proj.lora_B"], lora_scaling, rt)
-    qkv = rt(linear(x, w_in, p[pre + "attn.in_proj_bias"], rt))
+    qkv = rt(linear(x, w_in, p[pre + "attn.in_proj_bias"], rt, fp8=True))
     q, k, v = qkv.chunk(3, dim=-1)                                   # lora.py:840
 
     def heads(t):                                                     # lora.py:1002-1006
@@ -262,8 +331,9 @@ def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, ma
     else:
         x = x + a
     h2 = rt(layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"]))
-    f = rt(quick_gelu(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt)))
-    m = linear(f, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"], rt)
+    f = rt(quick_gelu(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt,
+                             fp8=True)))
+    m = linear(f, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"], rt, fp8=True)
     if variant == "adapter":
         m1 = None if masks is None else masks[1]
         x = x + adapter(rt(m), p, pre, dropout_mask=m1, rt=rt)

@@ -1,0 +1,124 @@
+"""Block-scaled fp8 path on the MI355X (BASELINE config 5): the quantiser against the oracle's
+restatement of the OCP MX e4m3 format bit for bit, and the fp8 MFMA GEMM (gemm8_kernel<., true>)
+against the oracle's dequantised product.
+
+Tolerances: quantised codes and scale bytes bit-exact; the GEMM on integer data in [-8, 8]
+(every value exactly representable after scaling) bit-exact; on random data the f32 output
+within 3e-5 relative-norm of the fp32 product of the oracle's dequantised operands (measured
+1.0e-5: the scaled MFMA's internal sum over its 128 k is not an IEEE f32 fma chain — an fp32
+CPU product of the same operands differs from the exact sum by ~1e-7); bf16-output
+epilogues 4e-3."""
+import pytest
+import torch
+
+from oracle import clip_oracle as o
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from lcclip import ops as _ops
+    return _ops
+
+
+def gpu_scales(fm):
+    """[K/128, rows_pad, 4] -> [rows, K/32] (the oracle's layout)."""
+    s = fm.scales.permute(1, 0, 2).reshape(fm.scales.shape[1], -1)
+    return s[:fm.rows]
+
+
+def ranged(rows, K, g, dev):
+    """Random data whose 32-blocks span 10^-4 .. 10^4 in magnitude, with all-zero blocks,
+    exact powers of two and values that saturate after scaling."""
+    x = torch.randn(rows, K, generator=g, device=dev)
+    mag = 10 ** (torch.rand(rows, K // 32, 1, generator=g, device=dev) * 8 - 4)
+    x = (x.view(rows, K // 32, 32) * mag).view(rows, K)
+    x[0, :32] = 0
+    x[1, :32] = 2.0 ** torch.arange(-10, 22, device=dev).float()
+    x[2, 32:64] = 448.0 * 3
+    return x
+
+
+@pytest.mark.parametrize("rows,K,src", [(300, 768, "bf16"), (513, 3072, "f32"), (64, 128, "f32T")])
+def test_quant_fp8_bitexact(ops, dev, rows, K, src):
+    g = torch.Generator(device=dev).manual_seed(rows + K)
+    x = ranged(rows, K, g, dev)
+    if src == "bf16":
+        x = x.to(BF)
+        fm = ops.quant_fp8(x)
+    elif src == "f32":
+        fm = ops.quant_fp8(x)
+    else:  # quantise x through its transpose view (the W^T staging of the dX weights)
+        xt = x.t().contiguous()
+        fm = ops.quant_fp8(xt, transpose=True)
+    codes, scales, _ = o.quant_fp8(x.float().cpu())
+    assert fm.scales.shape == (K // 128, (rows + 255) // 256 * 256, 4)
+    assert torch.equal(gpu_scales(fm).cpu(), scales)
+    assert torch.equal(fm.data.cpu(), codes)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 128), (4096 + 197, 768, 768), (1000, 2304, 3072),
+                                   (50432 // 4, 3072, 768)])
+def test_gemm_fp8_exact_integers(ops, dev, M, N, K):
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = torch.randint(-8, 9, (M, K), device=dev, generator=g).float()
+    B = torch.randint(-8, 9, (N, K), device=dev, generator=g).float()
+    Aq, Bq = ops.quant_fp8(A), ops.quant_fp8(B)
+    out = torch.full((M, N), float("nan"), device=dev)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_F32, out)
+    assert torch.equal(out, A @ B.t())
+
+
+@pytest.mark.parametrize("M,N,K", [(2 * 256 + 77, 768, 768), (50432, 768, 3072),
+                                   (12800, 2304, 768)])
+def test_gemm_fp8_vs_oracle(ops, dev, M, N, K):
+    """Random operands (the split-K tail path at M = 50 432, N = 768)."""
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N)
+    A = torch.randn(M, K, device=dev, generator=g).to(BF)
+    B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5)
+    bias = torch.randn(N, device=dev, generator=g)
+    Aq, Bq = ops.quant_fp8(A), ops.quant_fp8(B)
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_F32, out, bias=bias)
+    rows = slice(0, min(M, 4096))  # oracle product on a row slice (CPU time)
+    ref = o.fp8_round(A[rows].float().cpu()) @ o.fp8_round(B.cpu()).t() + bias.cpu()
+    assert rel(out[rows].cpu(), ref) < 3e-5
+    # the rest of the rows against the GPU's own dequantised operands
+    deqA = torch.from_numpy(o.quant_fp8(A[-4096:].float().cpu())[2].numpy()).to(dev)
+    ref2 = deqA @ o.fp8_round(B.cpu()).to(dev).t() + bias
+    assert rel(out[-4096:], ref2) < 3e-5
+
+
+def test_gemm_fp8_epilogues(ops, dev):
+    M, N, K = 4096 + 131, 3072, 768
+    g = torch.Generator(device=dev).manual_seed(11)
+    A = torch.randn(M, K, device=dev, generator=g)
+    B = torch.randn(N, K, device=dev, generator=g) * K ** -0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    Aq, Bq = ops.quant_fp8(A), ops.quant_fp8(B)
+    ref = (o.fp8_round(A.cpu()) @ o.fp8_round(B.cpu()).t()).to(dev)
+    o16 = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_BF16, o16, bias=bias)
+    assert rel(o16, ref + bias) < 4e-3
+    res = torch.randn(M, N, device=dev, generator=g)
+    o32 = torch.empty(M, N, device=dev)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_RESID, o32, bias=bias, aux=res)
+    assert rel(o32, ref + bias + res) < 1e-5
+    gd = torch.empty(M, N, device=dev, dtype=BF)
+    gl = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_GELU_D, gd, bias=bias, out1=gl)
+    pre = ref + bias
+    s = torch.sigmoid(1.702 * pre)
+    assert rel(gl, pre * s) < 4e-3
+    assert rel(gd, s * (1 + 1.702 * pre * (1 - s))) < 4e-3
+    aux = torch.randn(M, N, device=dev, generator=g).to(BF)
+    om = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_MUL, om, alpha=0.5, aux=aux)
+    assert rel(om, 0.5 * ref * aux.float()) < 4e-3

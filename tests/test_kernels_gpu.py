@@ -36,7 +36,7 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 11])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 11])
 def test_gemm_nt_every_tile_exact(ops, dev, tile):
     """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
     the fused QuickGELU-derivative epilogue against torch at bf16 tolerance."""
@@ -111,7 +111,18 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
                                    (296 * 256 - 100, 256, 2048)])
-def test_gemm_splitk_tail(ops, dev, M, N, K):
+@pytest.mark.parametrize("tile", [0, 8])
+def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
+    from lcclip import _lib
+    lib = _lib.load()
+    assert lib.lc_gemm_set_tile(tile) == 0
+    try:
+        _splitk_tail(ops, dev, M, N, K)
+    finally:
+        lib.lc_gemm_set_tile(0)
+
+
+def _splitk_tail(ops, dev, M, N, K):
     """The split-K tail of the 256x256 ping-pong GEMM (lc_gemm_nt_ws): these shapes leave the
     last round over 256 CUs at most half full (591 / 2364 / 296 tiles), so their tail tiles are
     summed from 3-4 K-slices. Small integers: every partial sum is exact in f32, so the result

@@ -298,7 +298,7 @@ def test_text_cache_freed_tokens_not_stale(golden, dev):
     t2 = OnlineTrainer(make_wrapper(sdi, "adapter", "image", dev))
     t2._cacheable = lambda: False
     other = tok.clone()
-    other[:, 1] = (other[:, 1] + 17) % 49000 + 256  # different class names, same shape
+    other[:, 1] = (other[:, 1] + 17) % 256 + 1  # other class names (ids < the TINY vocab 512)
     t1.forward_backward(img, y, tok.clone())          # temporary: freed after the call
     l1, p1 = t1.forward_backward(img, y, other.clone())
     l2, p2 = t2.forward_backward(img, y, other)

@@ -1,7 +1,8 @@
 """GEMM microbenchmark on the ViT-B/16 step's shapes (dev tool): lc_gemm_nt tile variants,
 random bf16 operands, HIP-event timing on the launch stream, interleaved rounds.
 
-  VARIANTS=1,5,5n  (5n = ping-pong without the split-K workspace)   SQUARE=1 adds 4096^3/8192^3
+  VARIANTS=1,5,5n,8,f8  (5n = ping-pong without the split-K workspace, 8 = phase-interleaved
+  bf16 kernel, f8 = its block-scaled fp8 form on pre-quantised operands)   SQUARE=1 adds 4096^3/8192^3
 """
 import os
 import sys
@@ -40,8 +41,16 @@ o1 = torch.empty(Mmax * Nmax, device=dev, dtype=torch.bfloat16)
 aux = torch.randn(Mmax * Nmax, device=dev).to(torch.bfloat16)
 
 
+_q = {}
+
+
 def launch(v, m, N, K, epi, a, b, out0, kw):
-    if v.endswith("n"):  # no split-K workspace
+    if v == "f8":
+        key = (m, N, K)
+        if key not in _q:
+            _q[key] = (ops.quant_fp8(a), ops.quant_fp8(b))
+        ops.gemm_nt_fp8(*_q[key], epi, out0, **kw)
+    elif v.endswith("n"):  # no split-K workspace
         out1, ax, bs = kw.get("out1"), kw.get("aux"), kw.get("bias")
         call("lc_gemm_nt", stream_of(a), epi, m, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(bs), 1.0, ptr(out0), N, ptr(out1), N if out1 is not None else 0, ptr(ax),
@@ -55,8 +64,8 @@ reps = int(os.environ.get("REPS", 10))
 for rnd in range(3):
     for name, m, N, K, epi in SHAPES:
         for v in VARIANTS:
-            t = int(v.rstrip("n"))
-            if t in (3, 5, 6, 7) and N % 256:
+            t = 8 if v == "f8" else int(v.rstrip("n"))
+            if t in (3, 5, 6, 7, 8) and N % 256:
                 continue
             lib.lc_gemm_set_tile(t)
             a = A[:m, :K]

@@ -5,8 +5,9 @@ usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json>
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reports half the
 bytes of a wide coalesced streaming read, so read_bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB)
 is exact for 16-B-per-lane stores. Kernels are keyed by their short name and grid size (one
-entry per launch shape); the 'families' section aggregates the 256x256 ping-pong GEMM launches
-(gemm_pp_kernel<EPI>, every epilogue, the dominant kernel bench.py reports)."""
+entry per launch shape); the 'families' section aggregates the 256x256 GEMM launches per kernel
+family (gemm8_kernel bf16 = the dominant kernel bench.py reports, its fp8 form, and the older
+ping-pong gemm_pp_kernel), every epilogue."""
 import collections
 import csv
 import glob
@@ -46,11 +47,16 @@ def main():
         name, grid = key
         out["kernels"][f"{name}|grid={grid}"] = {"launches": max(len(f), len(w)), "read_bytes": rd,
                                                  "write_bytes": wr}
-        if name.startswith("gemm_pp_kernel") and rd is not None and wr is not None:
+        family = None
+        if name.startswith("gemm_pp_kernel"):
+            family = "gemm_pp_kernel"
+        elif name.startswith("gemm8_kernel"):
+            family = "gemm8_kernel_fp8" if "true" in name else "gemm8_kernel_bf16"
+        if family and rd is not None and wr is not None:
             n = min(len(f), len(w))
-            fam["gemm_pp_kernel"][0] += n
-            fam["gemm_pp_kernel"][1] += rd * n
-            fam["gemm_pp_kernel"][2] += wr * n
+            fam[family][0] += n
+            fam[family][1] += rd * n
+            fam[family][2] += wr * n
     for k, (n, rd, wr) in fam.items():
         out["families"][k] = {"launches": n, "read_bytes_per_launch": rd / n,
                               "write_bytes_per_launch": wr / n,
