@@ -19,6 +19,12 @@ layout is internal and not observable):
 Frozen weights are staged once as bf16 in both [out,in] and [in,out] layouts (forward and dX
 GEMMs are both A @ B^T); LoRA blocks re-merge W + s*B@A into those buffers each step.
 The backbone is frozen: backward produces input gradients and PEFT parameter gradients only.
+
+precision='fp8' (BlockStack attribute; MaPLe's image tower under BASELINE config 5): the QKV,
+c_fc and c_proj GEMMs, forward and input-gradient, run as block-scaled e4m3 GEMMs on the fp8
+MFMA (ops.gemm_nt_fp8). Their frozen weights are quantised once per checkpoint in both layouts
+(from the f32 master, or from the bf16 LoRA merge), their activation / gradient operands at the
+call; out-projection, attention, LayerNorm and the residual stream stay as in bf16 mode.
 """
 from __future__ import annotations
 
@@ -68,6 +74,7 @@ class BlockStack:
         self.staged = [StagedBlock() for _ in self.blocks]
         # optional int64 device tensor: RNG epoch added to every dropout seed (graph replay)
         self.seed_dev = None
+        self.precision = "bf16"  # 'bf16' | 'fp8' (QKV / c_fc / c_proj on the fp8 MFMA)
 
     # ------------------------------------------------------------------ weight staging
     def trainable_params(self):
@@ -144,6 +151,38 @@ class BlockStack:
         # the adapter weights of every block change at each optimizer step: one launch for all
         if casts:
             ops.cast_weights(casts)
+        if self.precision == "fp8":
+            self._stage_fp8()
+
+    # frozen GEMM weights quantised to the fp8 operand format, both layouts
+    FP8_WEIGHTS = ("wqkv", "wqkvT", "wfc", "wfcT", "wpr", "wprT")
+
+    def _stage_fp8(self):
+        for blk, st in zip(self.blocks, self.staged):
+            D = blk.attn.in_proj_weight.shape[1]
+            if D % 256:
+                raise ValueError(f"precision='fp8' needs a width that is a multiple of 256 (got {D}): "
+                                 "the fp8 GEMM tiles N in 256-column blocks")
+            key = (st.frozen_key, st.peft_key)
+            if getattr(st, "q_key", None) == key:
+                continue
+            attn, mlp = blk.attn, blk.mlp
+            if self.variant == "lora":  # the per-step merged weights (bf16, both layouts)
+                src = {"wqkv": (st.wqkv, False), "wqkvT": (st.wqkvT, False)}
+            else:
+                w = attn.in_proj_weight.detach()
+                src = {"wqkv": (w, False), "wqkvT": (w, True)}
+            wf, wp = mlp.c_fc.weight.detach(), mlp.c_proj.weight.detach()
+            src.update(wfc=(wf, False), wfcT=(wf, True), wpr=(wp, False), wprT=(wp, True))
+            st.q = {name: ops.quant_fp8(t, transpose=tr) for name, (t, tr) in src.items()}
+            st.q_key = key
+
+    def _gemm(self, st, name, A, epi, out0, **kw):
+        """A [M, K] bf16 @ (staged weight `name`)^T: the bf16 GEMM, or in fp8 mode for the QKV /
+        c_fc / c_proj weights the fp8 GEMM on A quantised here."""
+        if self.precision == "fp8" and name in self.FP8_WEIGHTS:
+            return ops.gemm_nt_fp8(ops.quant_fp8(A), st.q[name], epi, out0, **kw)
+        return ops.gemm_nt(A, getattr(st, name), epi, out0, **kw)
 
     @staticmethod
     def _stage_lora(st, name, A, B):
@@ -207,7 +246,7 @@ class BlockStack:
             h1 = _empty((Mx, D), BF16, dev) if (save and self.variant == "lora") else th
             ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
             qkv = _empty((Mx, 3 * D), BF16, dev)
-            ops.gemm_nt(h1, st.wqkv, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
+            self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
             O = _empty((Mx, D), BF16, dev)
             lse = _empty((n_seq * H, Lx), F32, dev)
             ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
@@ -229,21 +268,21 @@ class BlockStack:
             ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
             pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
-            ops.gemm_nt(th, st.wfc, EPI_GELU_D if save else EPI_GELU, pre,
-                        bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
+            self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
+                       bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
             x_out = _empty((Mx, D), F32, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 seed2 = next(_seed_counter) * 0x9E3779B1
                 z2 = _empty((Mx, D), BF16, dev)
-                ops.gemm_nt(tmp_g[:Mx], st.wpr, EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
+                self._gemm(st, "wpr", tmp_g[:Mx], EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
                 hd2 = _empty((Mx, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
                                 s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
-                ops.gemm_nt(tmp_g[:Mx], st.wpr, EPI_RESID, x_out, bias=blk.mlp.c_proj.bias,
-                            aux=x_mid)
+                self._gemm(st, "wpr", tmp_g[:Mx], EPI_RESID, x_out, bias=blk.mlp.c_proj.bias,
+                           aux=x_mid)
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
                          mean2=mean2, rstd2=rstd2, gd=pre, P=P)
@@ -321,8 +360,8 @@ class BlockStack:
                 dY = self._adapter_bwd(blk, st, gxb, s["hd2"], s["z2"], s["keep"], dz[:Mx], grads)
             else:
                 dY = gxb
-            ops.gemm_nt(dY, st.wprT, EPI_MUL, da[:Mx], aux=s["gd"])
-            ops.gemm_nt(da[:Mx], st.wfcT, EPI_BF16, dh[:Mx])
+            self._gemm(st, "wprT", dY, EPI_MUL, da[:Mx], aux=s["gd"])
+            self._gemm(st, "wfcT", da[:Mx], EPI_BF16, dh[:Mx])
             ops.layernorm_bwd(dh[:Mx], s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight,
                               dx_mid[:Mx], dx_midb[:Mx], dres=gx)
             # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))
@@ -347,7 +386,7 @@ class BlockStack:
             if first:
                 self._layer_done(li, grad_stream, on_layer)
                 break
-            ops.gemm_nt(dqkv[:Mx], st.wqkvT, EPI_BF16, dh[:Mx])
+            self._gemm(st, "wqkvT", dqkv[:Mx], EPI_BF16, dh[:Mx])
             ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
                               oxb, dres=dx_mid[:Mx])
             ev = self._layer_done(li, grad_stream, on_layer)

@@ -12,7 +12,10 @@ learned context at rows 1..n_ctx, the image sequence gets proj(ctx) appended bef
 returns the gradients of every prompt row through the frozen blocks.
 
 Deviations: compute is bf16 MFMA with fp32 accumulation and an fp32 residual stream (the
-reference casts the visual prompts to fp16, model.py:374 and :569). Tokenisation needs a BPE
+reference casts the visual prompts to fp16, model.py:374 and :569). precision='fp8' (BASELINE
+config 5) runs the image tower's frozen QKV / c_fc / c_proj GEMMs, forward and input-gradient,
+as block-scaled e4m3 GEMMs on the fp8 MFMA (engine.BlockStack, precision attribute); the text
+tower (C x 77 rows: too few for the 256x256 fp8 tiles) stays bf16. Tokenisation needs a BPE
 tokenizer callable (tokenizer=); without one, set_tokenized_prompts() takes token ids and the
 context is initialised from the reference's random branch (maple.py:95-98), or from
 ctx_init_tokens (the ids of "a bad photo of a") as its ctx_init branch does.
@@ -117,7 +120,7 @@ class MaPLe(nn.Module):
     """maple.py:143-253."""
 
     def __init__(self, model_name="ViT-B/16", n_ctx=3, device="cpu", tokenizer=None,
-                 ctx_init_tokens=None, arch_overrides=None, clip_model=None):
+                 ctx_init_tokens=None, arch_overrides=None, clip_model=None, precision="bf16"):
         super().__init__()
         self.device = device
         if clip_model is None:
@@ -141,14 +144,23 @@ class MaPLe(nn.Module):
         self.tokenized_prompts = None
         self.current_class_names = []
         self.prompt_prefix = self.prompt_learner.prompt_prefix
+        self.set_precision(precision)
         if device is not None and str(device) != "cpu":
             self.to(device)
 
+    def set_precision(self, precision):
+        """'bf16' or 'fp8' for the image tower's frozen GEMMs."""
+        if precision not in ("bf16", "fp8"):
+            raise ValueError("precision must be 'bf16' or 'fp8'")
+        self.precision = precision
+        self.image_encoder.tower.stack.precision = precision
+        return self
+
     @classmethod
-    def from_state_dict(cls, state_dict, n_ctx=3, device=None, **kwargs):
+    def from_state_dict(cls, state_dict, n_ctx=3, device=None, precision="bf16", **kwargs):
         from .model import build_model
         bb = build_model(dict(state_dict), {"method": "maple", "peft_encoder": "none"})
-        return cls(n_ctx=n_ctx, device=device, clip_model=bb, **kwargs)
+        return cls(n_ctx=n_ctx, device=device, clip_model=bb, precision=precision, **kwargs)
 
     def update_class_names(self, new_class_names):
         """maple.py:178-187 (needs the tokenizer)."""

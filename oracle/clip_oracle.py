@@ -645,8 +645,11 @@ TINY_MVP = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=6, vision
 # MaPLe (models/maple.py + models/maple_clip/model.py, BASELINE config 5): frozen backbone,
 # multi-modal prompts. mp: {'ctx' [n_ctx, Dt], 'proj.weight' [Dv, Dt], 'proj.bias' [Dv],
 # 'text.{i}' [n_ctx, Dt], 'vproj.{i}.weight' [Dv, Dt], 'vproj.{i}.bias' [Dv]} for i < depth-1.
-def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, rt=identity):
-    """MaPLe.forward (maple.py:208-251) -> logits [B, C] (no softmax)."""
+def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, rt=identity,
+                  rt_img=None):
+    """MaPLe.forward (maple.py:208-251) -> logits [B, C] (no softmax). rt_img: the image tower's
+    rounding hook when it differs from the text tower's (fp8 image tower: fp8_rounding())."""
+    rt_img = rt if rt_img is None else rt_img
     C = tokens.shape[0]
     emb = p["token_embedding.weight"][tokens]                                  # maple.py:200-203
     prefix, suffix = emb[:, :1], emb[:, 1 + n_ctx:]                            # :205-206
@@ -673,7 +676,7 @@ def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, r
     W, P = cfg.vision_width, cfg.vision_patch_size
     g = cfg.grid
     patches = img.reshape(N, 3, g, P, g, P).permute(0, 2, 4, 1, 3, 5).reshape(N, g * g, 3 * P * P)
-    xi = linear(patches, p["visual.conv1.weight"].reshape(W, -1), None, rt)
+    xi = linear(patches, p["visual.conv1.weight"].reshape(W, -1), None, rt_img)
     cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
     xi = torch.cat([cls, xi], dim=1) + p["visual.positional_embedding"]
     xi = torch.cat([xi, shared.unsqueeze(0).expand(N, -1, -1)], dim=1)        # :568-570
@@ -682,9 +685,9 @@ def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, r
     for i, pre in enumerate(vis):
         if 1 <= i <= len(deep_vis):
             xi = torch.cat([xi[:, :-n_ctx], deep_vis[i - 1].unsqueeze(0).expand(N, -1, -1)], dim=1)
-        xi = block(xi, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
-    xi = rt(layer_norm(xi[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
-    img_f = linear(xi, p["visual.proj"].t(), None, rt)
+        xi = block(xi, p, pre, cfg.vision_heads, False, "vanilla", rt=rt_img)
+    xi = rt_img(layer_norm(xi[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
+    img_f = linear(xi, p["visual.proj"].t(), None, rt_img)
     logits, _, _ = clip_logits(img_f, txt_f, p["logit_scale"])                # :244-250
     return logits
 
@@ -712,6 +715,11 @@ MAPLE_TO_MODULE = {"ctx": "prompt_learner.ctx", "proj.weight": "prompt_learner.p
                    "vproj.0.bias": "prompt_learner.compound_prompt_projections.0.bias",
                    "vproj.1.weight": "prompt_learner.compound_prompt_projections.1.weight",
                    "vproj.1.bias": "prompt_learner.compound_prompt_projections.1.bias"}
+
+# fp8 image tower needs widths in multiples of 256 (the fp8 GEMM's N tiles)
+TINY_MAPLE8 = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=4, vision_width=256,
+                         vision_patch_size=16, context_length=77, vocab_size=512,
+                         transformer_width=64, transformer_heads=1, transformer_layers=3)
 
 TINY_MAPLE = ClipConfig(embed_dim=64, image_resolution=64, vision_layers=4, vision_width=128,
                         vision_patch_size=16, context_length=77, vocab_size=512,

@@ -77,3 +77,80 @@ def test_maple_vit_b16_shapes(dev):
     run_case(cfg, o.synthetic_state_dict(cfg, seed=43), o.maple_params(cfg, seed=3),
              o.synthetic_images(2, 224, seed=7), o.synthetic_tokens(4, 77, seed=7),
              torch.tensor([1, 3]), dev, "maple_vit_b16")
+
+
+# ----------------------------------------------------------------------------- fp8 (config 5)
+def run_case_fp8(cfg, sd, mp, img, tok, y, dev, tag, tol):
+    """MaPLe with precision='fp8' (image tower QKV / c_fc / c_proj on the block-scaled fp8 MFMA,
+    forward and input-gradient) vs the oracle's fp8 rounding mode (oracle.fp8_rounding: the same
+    e4m3 / E8M0 quantisation at the same GEMM operands, bf16 elsewhere) and vs plain fp32.
+    The quantiser and the fp8 GEMM themselves are pinned bit-exactly in tests/test_fp8_gpu.py;
+    through a whole tower the two sides' quantiser INPUTS differ by bf16 rounding (different
+    accumulation orders), and a 2^-8 input difference flips ~3 % of the e4m3 codes (2^-3
+    steps), so the GPU-vs-fp8-oracle gap is a fraction of the fp8 error itself (measured: 0.56x
+    at ViT-B/16 shapes, 0.58x on the tiny tower). Tolerances per case in `tol` (cosine units of
+    the logits = logit / exp(logit_scale); gradient rel-norm), ~2x the measured values."""
+    from lcclip.maple import MaPLe
+    rt8 = o.fp8_rounding()
+    with torch.no_grad():
+        l32 = o.maple_forward(img, tok, sd, cfg, mp)
+        l8 = o.maple_forward(img, tok, sd, cfg, mp, rt=o.round_bf16, rt_img=rt8)
+    g32 = {k: v.clone().requires_grad_(True) for k, v in mp.items()}
+    F.cross_entropy(o.maple_forward(img, tok, sd, cfg, g32), y).backward()
+    g8 = {k: v.clone().requires_grad_(True) for k, v in mp.items()}
+    F.cross_entropy(o.maple_forward(img, tok, sd, cfg, g8, rt=o.round_bf16, rt_img=rt8),
+                    y).backward()
+
+    m = MaPLe.from_state_dict(sd, device=dev, precision="fp8")
+    params = dict(m.named_parameters())
+    with torch.no_grad():
+        for k, name in o.MAPLE_TO_MODULE.items():
+            params[name].copy_(mp[k])
+    m.set_tokenized_prompts(tok.to(dev))
+    logits = m(img.to(dev))
+    F.cross_entropy(logits, y.to(dev)).backward()
+    torch.cuda.synchronize()
+    ls = math.exp(sd["logit_scale"].item())
+    met = dict(cos_err_vs_fp32=((logits.detach().cpu() - l32).abs().max() / ls).item(),
+               cos_err_vs_fp8=((logits.detach().cpu() - l8).abs().max() / ls).item(),
+               fp8_oracle_vs_fp32=((l8 - l32).abs().max() / ls).item())
+    for k, name in o.MAPLE_TO_MODULE.items():
+        met[f"grad_{k}_rel_fp8"] = rel(params[name].grad, g8[k].grad)
+        met[f"grad_{k}_rel_fp32"] = rel(params[name].grad, g32[k].grad)
+    record(test=tag, **met)
+    assert met["cos_err_vs_fp8"] < tol["cos_fp8"] and met["cos_err_vs_fp32"] < tol["cos_fp32"], met
+    for k in o.MAPLE_TO_MODULE:
+        assert met[f"grad_{k}_rel_fp8"] < tol["grad_fp8"], (k, met)
+        assert met[f"grad_{k}_rel_fp32"] < tol["grad_fp32"], (k, met)
+
+
+def test_maple_fp8_tiny(dev):
+    cfg = o.TINY_MAPLE8
+    run_case_fp8(cfg, o.synthetic_state_dict(cfg, seed=51), o.maple_params(cfg, seed=4),
+                 o.synthetic_images(3, cfg.image_resolution, seed=8),
+                 o.synthetic_tokens(4, 77, seed=8, vocab=cfg.vocab_size), torch.tensor([0, 2, 3]),
+                 dev, "maple_fp8_tiny",
+                 # measured: cos 1.2e-2 / 1.8e-2 (the fp8 oracle itself is 2.0e-2 from fp32);
+                 # gradients 0.06-0.11 / 0.10-0.16
+                 dict(cos_fp8=2.5e-2, cos_fp32=4e-2, grad_fp8=0.2, grad_fp32=0.3))
+
+
+def test_maple_fp8_vit_b16_shapes(dev):
+    """ViT-B/16 + 12-layer text tower, image L = 200, B = 2, C = 4, fp8 image tower."""
+    cfg = o.VIT_B16
+    run_case_fp8(cfg, o.synthetic_state_dict(cfg, seed=43), o.maple_params(cfg, seed=3),
+                 o.synthetic_images(2, 224, seed=7), o.synthetic_tokens(4, 77, seed=7),
+                 torch.tensor([1, 3]), dev, "maple_fp8_vit_b16",
+                 # measured: cos 2.2e-3 / 3.2e-3 (the fp8 oracle itself is 4.0e-3 from fp32);
+                 # gradients 0.05-0.09 / 0.08-0.14
+                 dict(cos_fp8=5e-3, cos_fp32=8e-3, grad_fp8=0.15, grad_fp32=0.25))
+
+
+def test_maple_fp8_rejects_narrow_tower(dev):
+    """No silent bf16 fallback: an image width that the fp8 tiles cannot cover raises."""
+    from lcclip.maple import MaPLe
+    cfg = o.TINY_MAPLE  # vision width 128
+    m = MaPLe.from_state_dict(o.synthetic_state_dict(cfg, seed=1), device=dev, precision="fp8")
+    m.set_tokenized_prompts(o.synthetic_tokens(2, 77, seed=1, vocab=cfg.vocab_size).to(dev))
+    with pytest.raises(ValueError, match="fp8"):
+        m(o.synthetic_images(1, cfg.image_resolution, seed=1).to(dev))

@@ -1,7 +1,9 @@
 """MaPLe step throughput (BASELINE config 5 model, n_ctx 3, depth 3) on one MI355X: both towers
 fwd + bwd to the prompt learner (the text tower is trained through its prompts, so it is not
 cached), CE on the logits, AdamW. scripts/maple.sh:26-31 uses batch 64; C = 100 classes.
-Synthetic 224x224 inputs, random-init ViT-B/16 weights. Prints one JSON line."""
+Synthetic 224x224 inputs, random-init ViT-B/16 weights. PREC=bf16|fp8|both (default both: the
+image tower's frozen QKV / c_fc / c_proj GEMMs in bf16 or on the block-scaled fp8 MFMA, as
+BASELINE config 5 names). Prints one JSON line per precision."""
 import json
 import os
 import sys
@@ -19,10 +21,16 @@ WARM = int(os.environ.get("WARM", 3))
 
 
 def main():
+    for prec in (("bf16", "fp8") if os.environ.get("PREC", "both") == "both"
+                 else (os.environ["PREC"],)):
+        run(prec)
+
+
+def run(prec):
     from lcclip.maple import MaPLe
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    m = MaPLe("ViT-B/16", n_ctx=3, device=dev)
+    m = MaPLe("ViT-B/16", n_ctx=3, device=dev, precision=prec)
     m.train()
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand(B, 3, 224, 224, device=dev, generator=g)
@@ -52,7 +60,9 @@ def main():
     dt = (time.perf_counter() - t0) / STEPS
     print(json.dumps({"workload": "maple ViT-B/16 multi-modal prompts (config 5 model)",
                       "batch": B, "classes": C, "ms_per_step": round(dt * 1e3, 3),
-                      "images_per_s": round(B / dt, 1), "dtype": "bf16 (config 5 names fp8)",
+                      "images_per_s": round(B / dt, 1),
+                      "dtype": "fp8 e4m3 (image QKV/c_fc/c_proj fwd+dX), bf16 elsewhere"
+                      if prec == "fp8" else "bf16",
                       "data": "synthetic"}), flush=True)
 
 
