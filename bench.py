@@ -58,7 +58,7 @@ def routes_to_pp(M, N, K, epi):
     """The lc_gemm_nt tile selector's rule for the 256x256 phase-interleaved kernel (gemm.hip,
     lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step. The c_proj dX x
     QuickGELU' GEMM (EPI_MUL, K <= 1024, N >= 2048) goes to the 4-wave kernel instead."""
-    g8 = N % 128 == 0 and M >= 4096 and N % 256 == 0
+    g8 = N % 128 == 0 and M >= 4096 and N % 256 == 0 and (M + 255) // 256 * (N // 256) >= 256
     from lcclip.ops import EPI_MUL
     return g8 and not (epi == EPI_MUL and K <= 1024 and N >= 2048)
 

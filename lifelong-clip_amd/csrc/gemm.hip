@@ -1565,9 +1565,10 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     // measured on the ViT-B/16 step shapes (tools/bench_gemm.py, M = 50 432): the 256x256
     // phase-interleaved kernel beats the ping-pong one on every shape (776-1113 vs 743-1044 TF)
     // and the 128x128 kernel on N = K = 768 (858 vs ~780 TF); 128x128 at 2 workgroups/CU for
-    // the small-M (text tower) launches
+    // launches with fewer 256x256 tiles than CUs (text tower, MaPLe's 64-image batch at N =
+    // 768: 150 tiles) — those would leave CUs idle
     if (N % 128 != 0) tile = 4;
-    else if (M >= 4096 && N % 256 == 0) tile = 8;
+    else if (M >= 4096 && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= cu_count()) tile = 8;
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 289 vs 295 us (bench_gemm.py)
     if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048) tile = 7;

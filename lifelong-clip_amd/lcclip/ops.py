@@ -74,8 +74,10 @@ class Fp8Mat:
         pad = (rows + 255) // 256 * 256
         self.rows, self.K = rows, K
         self.data = data if data is not None else torch.empty((rows, K), dtype=FP8, device=device)
-        self.scales = scales if scales is not None else torch.zeros((K // 128, pad, 4), dtype=FP8,
-                                                                  device=device)
+        # rows >= `rows` of the scale buffer are never written: the GEMM reads them only for
+        # tail rows it computes and never stores
+        self.scales = scales if scales is not None else torch.empty((K // 128, pad, 4), dtype=FP8,
+                                                                   device=device)
 
     @property
     def rows_pad(self):

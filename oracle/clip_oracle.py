@@ -430,8 +430,9 @@ def adamw_step(params, grads, state, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, wd=1
     return out
 
 
-def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-4):
+def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-4, state=None):
     """methods/adapter_clip.py:86-96 at p=0 dropout: fwd -> CE(probs) -> bwd -> AdamW.
+    state: the AdamW state carried across steps (None: a fresh optimizer).
     Returns (loss, probs, img_f, txt_f, grads, new_params)."""
     leaves = {n: t.detach().clone().requires_grad_(is_trainable(n)) for n, t in p.items()}
     probs, fi, ft = adapter_clip_forward(img, tokens, leaves, cfg, method, peft_encoder, rt)
@@ -440,8 +441,45 @@ def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-
     if not train:  # vanilla blocks: nothing is trainable (the freeze filter leaves no params)
         return loss.detach(), probs.detach(), fi.detach(), ft.detach(), {}, {}
     grads = dict(zip(train.keys(), torch.autograd.grad(loss, list(train.values()))))
-    new = adamw_step({n: t.detach() for n, t in train.items()}, grads, {}, lr=lr)
+    new = adamw_step({n: t.detach() for n, t in train.items()}, grads,
+                     {} if state is None else state, lr=lr)
     return loss.detach(), probs.detach(), fi.detach(), ft.detach(), grads, new
+
+
+def online_loop(task_batches, images, labels, class_tokens, p, cfg, method="adapter",
+                peft_encoder="both", online_iter=3, lr=5e-4, rt=identity):
+    """The online loop of methods/_trainer.py:320-357 + methods/adapter_clip.py:34-107, restated
+    for the trajectory parity test (replay memory off, visible_classes='batch', p = 0 dropout,
+    inputs already transformed). task_batches: per task, the list of sample-index lists the
+    sampler yields; class_tokens: [n_classes, L] token ids in class-id order.
+      online_before_task: a fresh AdamW per task (adapter_clip.py:115-127, Q14)
+      online_step: exposed classes += new labels (_trainer.py:404-413), the batch's class list
+                   = its distinct labels in first-seen order (adapter_clip.py:263-283), then
+                   online_iter x online_train on clones of the batch (:42-46)
+      online_train: y -> index in the batch class list (:75-76), tokens of that list (:84),
+                   fwd + CE-on-probs + bwd + AdamW (:86-96)
+    Returns [(loss, {trainable name: tensor after the step})] per optimizer step."""
+    params = {n: t.detach().clone() for n, t in p.items()}
+    exposed, out = [], []
+    for batches in task_batches:
+        state = {}
+        for b in batches:
+            ys = [int(v) for v in labels[b].tolist()]
+            for y in ys:
+                if y not in exposed:
+                    exposed.append(y)
+            batch_list = []
+            for y in ys:
+                if y not in batch_list:
+                    batch_list.append(y)
+            for _ in range(online_iter):
+                yi = torch.tensor([batch_list.index(y) for y in ys], dtype=torch.long)
+                tok = class_tokens[torch.tensor(batch_list)]
+                loss, _, _, _, _, new = train_step(images[b], tok, yi, params, cfg, method,
+                                                   peft_encoder, rt, lr, state)
+                params.update(new)
+                out.append((loss, {n: t.clone() for n, t in new.items()}))
+    return out
 
 
 # ----------------------------------------------------------------------------- train transform

@@ -1,0 +1,124 @@
+"""The online continual-learning loop (lcclip.online.OnlineLoop: methods/_trainer.py:320-357 +
+methods/adapter_clip.py:34-176) on the MI355X against the oracle's own restatement of that loop
+(oracle.clip_oracle.online_loop), step for step across a task boundary.
+
+Setup: TINY adapter-CLIP (both towers, p = 0 dropout, nonzero adapter up-projections), 4
+classes over 2 Si-Blurry tasks (N = 100 %: disjoint), 4 samples per task in one batch,
+online_iter = 3 -> 6 optimizer steps, AdamW rebuilt at the task boundary, inputs already
+model-shaped (no random transform: the trajectory must be deterministic on both sides).
+Tolerances (stated): per-step loss within 5e-3 of the bf16-rounding oracle; per-step parameter
+update (p_k - p_{k-1}, all trainables) cosine >= 0.97 and norm within 10 % of the oracle's —
+Adam's early steps are ~lr*sign(g), so elements with near-zero gradient may flip sign between
+bf16 and fp32 arithmetic; a missing optimizer reset at the boundary turns step 4's update into a
+momentum-smoothed one and fails both bounds (checked in the test)."""
+import pytest
+import torch
+
+from oracle import clip_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def make_wrapper(sd, dev):
+    from lcclip.adapter_clip import AdapterCLIP, set_adapter_dropout
+    w = AdapterCLIP.from_state_dict(sd, "adapter", "both", device=dev)
+    return set_adapter_dropout(w, 0.0)
+
+
+def setup(dev):
+    from lcclip.stream import ClassBook, SiBlurryStream
+    cfg = o.TINY
+    sd = o.synthetic_state_dict(cfg, "adapter", "both", seed=21)
+    imgs = o.synthetic_images(8, cfg.image_resolution, seed=4)
+    labels = torch.tensor([0, 1, 0, 1, 2, 3, 3, 2])
+    class_tokens = o.synthetic_tokens(4, 77, seed=12, vocab=cfg.vocab_size)
+    names = [f"class{i}" for i in range(4)]
+    stream = SiBlurryStream(labels.tolist(), 4, 2, m=0, n=100, rnd_seed=3)
+    book = ClassBook(names)
+
+    def tokenize(ns):
+        return class_tokens[torch.tensor([int(n[5:]) for n in ns])].to(dev)
+    return cfg, sd, imgs, labels, class_tokens, stream, book, tokenize
+
+
+def run_gpu(dev, lr, reset=True):
+    from lcclip import OnlineTrainer
+    from lcclip.online import OnlineLoop
+    cfg, sd, imgs, labels, class_tokens, stream, book, tokenize = setup(dev)
+    w = make_wrapper(sd, dev)
+    tr = OnlineTrainer(w, lr=lr)
+    if not reset:
+        tr.reset_optimizer = lambda: None
+    names = {id(p): n for n, p in w.model.named_parameters()}
+    order = [names[id(p)] for p in tr.params]
+    snaps = [tr.flat_p.clone()]
+    losses = []
+
+    def on_step(i, loss, acc):
+        losses.append(loss)
+        snaps.append(tr.flat_p.clone())
+    loop = OnlineLoop(tr, stream, book, imgs, labels, imgs, labels, tokenize, batch_size=4,
+                      online_iter=3, eval_period=4, on_step=on_step)
+    res = loop.run()
+    return res, losses, snaps, order, tr
+
+
+def record(**kw):
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(root, "gpurun_out", "parity_metrics.jsonl"), "a") as f:
+        f.write(json.dumps(kw) + "\n")
+
+
+def flat(d, order):
+    return torch.cat([d[n].reshape(-1).float() for n in order])
+
+
+def test_online_loop_trajectory_vs_oracle(dev):
+    lr = 2e-3
+    cfg, sd, imgs, labels, class_tokens, stream, book, _ = setup(dev)
+    res, losses, snaps, order, tr = run_gpu(dev, lr)
+    assert res["steps"] == 6 and len(losses) == 6
+    batches = [[stream.task_indices(t)] for t in range(2)]
+    assert all(len(b[0]) == 4 for b in batches)
+    ref = o.online_loop(batches, imgs, labels, class_tokens, sd, cfg, online_iter=3, lr=lr,
+                        rt=o.round_bf16)
+    assert len(ref) == 6
+    prev_ref = flat(sd, order)
+    met = []
+    for k, (rl, rp) in enumerate(ref):
+        cur_ref = flat({**{n: sd[n] for n in order}, **rp}, order)
+        d_ref = cur_ref - prev_ref
+        d_gpu = (snaps[k + 1] - snaps[k]).cpu()
+        cos = torch.nn.functional.cosine_similarity(d_gpu, d_ref, dim=0).item()
+        nrm = (d_gpu.norm() / d_ref.norm()).item()
+        met.append(dict(step=k + 1, loss_abs=abs(losses[k] - rl.item()), update_cos=cos,
+                        update_norm_ratio=nrm))
+        assert abs(losses[k] - rl.item()) < 5e-3, (k, losses[k], rl.item())
+        assert cos >= 0.97 and abs(nrm - 1) < 0.1, (k, cos, nrm)
+        prev_ref = cur_ref
+    record(test="online_loop_trajectory", steps=met, summary=res["summary"])
+    s = res["summary"]
+    assert 0.0 <= s["A_avg"] <= 1.0 and 0.0 <= s["A_last"] <= 1.0
+    assert len(res["eval_results"]["test_acc"]) == 2  # eval_period 4 over 8 samples
+    assert 0.0 <= s["A_auc"] <= 1.0
+    assert len(res["task_records"]["task_acc"]) == 2
+
+
+def test_online_loop_detects_missing_optimizer_reset(dev):
+    """The trajectory bound is sharp enough to see a skipped AdamW rebuild at the boundary."""
+    lr = 2e-3
+    cfg, sd, imgs, labels, class_tokens, stream, book, _ = setup(dev)
+    _, _, snaps, order, _ = run_gpu(dev, lr, reset=False)
+    batches = [[stream.task_indices(t)] for t in range(2)]
+    ref = o.online_loop(batches, imgs, labels, class_tokens, sd, cfg, online_iter=3, lr=lr,
+                        rt=o.round_bf16)
+    p3 = flat({**{n: sd[n] for n in order}, **ref[2][1]}, order)
+    p4 = flat({**{n: sd[n] for n in order}, **ref[3][1]}, order)
+    d_ref = p4 - p3
+    d_gpu = (snaps[4] - snaps[3]).cpu()
+    cos = torch.nn.functional.cosine_similarity(d_gpu, d_ref, dim=0).item()
+    nrm = (d_gpu.norm() / d_ref.norm()).item()
+    assert cos < 0.97 or abs(nrm - 1) >= 0.1, (cos, nrm)
