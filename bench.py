@@ -164,7 +164,8 @@ def time_train_transform(B, dev, reps=20):
     from lcclip.transforms import TrainTransform
     x = torch.randint(0, 256, (B, 3, 32, 32), device=dev).float() / 255
     tf = TrainTransform.for_dataset("cifar100", generator=torch.Generator().manual_seed(0))
-    prm = tf.draw()
+    # a fixed two-op CIFAR10 sub-policy (AutoAugment kernel + resize/crop/flip/normalise kernel)
+    prm = ([("Equalize", 0.0), ("Rotate", 20.0)], 4, 4, True)
     out = tf(x, params=prm, layout="patches")
     st = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -174,9 +175,10 @@ def time_train_transform(B, dev, reps=20):
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
-    nbytes = x.numel() * 4 + out.numel() * 2
-    return {"kernel": "train_transform_kernel (quantise + resize 32->224 + pad-crop + flip + "
-                      "normalise, written as conv1 bf16 patch rows)",
+    nbytes = x.numel() * 4 * 3 + out.numel() * 2  # autoaug read + write, transform read; output
+    return {"kernel": "autoaug_kernel (uint8 quantise + Equalize + Rotate) then "
+                      "train_transform_lds_kernel (resize 32->224 + pad-crop + flip + normalise, "
+                      "written as conv1 bf16 patch rows)",
             "batch": B, "avg_launch_us": round(us, 2), "algorithmic_bytes": nbytes,
             "achieved_GBps": round(nbytes / (us * 1e-6) / 1e9, 1), "peak_GBps": PEAK_HBM / 1e9}
 

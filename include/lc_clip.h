@@ -163,6 +163,17 @@ int lc_train_transform(hipStream_t stream, int n, int C, int Hin, int Win, const
                        int pad, int crop_i, int crop_j, int flip, const float* mean_host,
                        const float* std_host, int quantize, int layout, int patch, void* out);
 
+/* AutoAugment (torchvision 0.16 AutoAugment, the 'autoaug' branch of methods/_trainer.py:215-229)
+ * on the uint8-quantised batch: x f32 [n, C, H, W] in [0, 1] -> out f32 = augmented uint8 / 255.
+ * n_ops (0..2) ops of one drawn sub-policy, shared by the batch (torchvision draws once per call):
+ * codes[i] in 0..9 (invert, brightness, color, contrast, sharpness blends, posterize, solarize,
+ * autocontrast, equalize, nearest affine) with 6 f32 parameters each in params (the host computes
+ * blend ratios, masks, thresholds and the rescaled inverse affine grid matrix, lcclip/transforms.py).
+ * C*H*W <= 12288 (CIFAR 32x32, TinyImageNet 64x64). Replaces: transforms.AutoAugment(policy)
+ * (methods/_trainer.py:217-228). */
+int lc_autoaugment(hipStream_t stream, int n, int C, int H, int W, const float* x, float* out,
+                   int n_ops, const int* codes, const float* params);
+
 /* f32 -> bf16 cast of n elements (weight staging). */
 int lc_cast_bf16(hipStream_t stream, long n, const float* src, void* dst);
 

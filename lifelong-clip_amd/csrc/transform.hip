@@ -235,3 +235,199 @@ int lc_train_transform(hipStream_t st, int n, int C, int Hin, int Win, const flo
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// AutoAugment ops on the uint8 batch (the 'autoaug' branch of methods/_trainer.py:215-229:
+// (x*255).type(uint8) -> transforms.AutoAugment(policy) -> .float()/255). torchvision draws one
+// sub-policy per call for the whole batch tensor; the host (lcclip/transforms.py) draws it and
+// passes the active ops, each restated here from torchvision 0.16's tensor functional ops:
+//   INVERT      255 - v
+//   BLEND       (c1 * v + c2 * other).clamp(0, 255) truncated to uint8 (_blend), with other =
+//               0 (adjust_brightness), the uint8-truncated grayscale (adjust_saturation), its
+//               per-image mean (adjust_contrast), or the 3x3 [1 1 1; 1 5 1; 1 1 1]/13 blur,
+//               rounded, borders kept (adjust_sharpness)
+//   POSTERIZE   v & mask;  SOLARIZE  v >= thr ? 255 - v : v
+//   AUTOCONTRAST per image+channel ((v - min) * (255 / (max - min))).clamp truncated (min = 0,
+//               scale = 1 where max == min; the scale is torch's reciprocal(max - min) * 255)
+//   EQUALIZE    per image+channel histogram LUT: step = (sum of the non-zero bins but the last)
+//               // 255; lut[k] = (cumsum[k-1] + step // 2) // step (lut[0] = 0), identity when
+//               step == 0
+//   AFFINE      nearest grid_sample (align_corners = False, zero fill) on torchvision's affine
+//               grid: base (x, y) = (j - W/2 + 0.5, i - H/2 + 0.5), g = (x r0 + y r1) + r2 /
+//               (x r3 + y r4) + r5 with the host's rescaled inverse matrix, source index =
+//               rint(((g + 1) * size - 1) / 2) (ShearX/Y, TranslateX/Y, Rotate)
+// One workgroup per image, the image resident in LDS (C*H*W <= 12288: CIFAR 32x32, Tiny-
+// ImageNet 64x64). f32 arithmetic is written op by op (no contraction) in torch's order so the
+// result is bit-identical to the oracle's restatement (oracle/clip_oracle.py autoaugment).
+namespace {
+
+enum { AA_INVERT = 0, AA_BLEND_ZERO = 1, AA_BLEND_GRAY = 2, AA_BLEND_MEAN = 3, AA_BLEND_BLUR = 4,
+       AA_POSTERIZE = 5, AA_SOLARIZE = 6, AA_AUTOCONTRAST = 7, AA_EQUALIZE = 8, AA_AFFINE = 9 };
+
+struct AugOps {
+  int n;
+  int code[2];
+  float p[2][6];
+};
+
+LC_DEV int trunc_u8(float v) {  // .clamp(0, 255).to(torch.uint8)
+  v = fminf(fmaxf(v, 0.f), 255.f);
+  return (int)v;
+}
+
+LC_DEV int gray_u8(int r, int g, int b) {  // rgb_to_grayscale(uint8): (0.2989r + 0.587g + 0.114b).to(uint8)
+  const float s = __fadd_rn(__fadd_rn(__fmul_rn(0.2989f, (float)r), __fmul_rn(0.587f, (float)g)),
+                            __fmul_rn(0.114f, (float)b));
+  return (int)s;
+}
+
+__global__ void __launch_bounds__(256)
+autoaug_kernel(int C, int H, int W, const float* __restrict__ x, float* __restrict__ out, AugOps ops) {
+  extern __shared__ int sm[];
+  const int HW = H * W, tot = C * HW;
+  int* a = sm;                 // current image
+  int* b = sm + tot;           // scratch image
+  int* hist = b + tot;         // [C][256] histogram / LUT
+  int* red = hist + 4 * 256;   // reductions: [0..3] min, [4..7] max, [8] gray sum
+  const int tid = threadIdx.x;
+  const float* src = x + (long)blockIdx.x * tot;
+  for (int k = tid; k < tot; k += blockDim.x) {
+    const float t = src[k] * 255.0f;  // (x * 255).type(torch.uint8)
+    int u = (int)t;
+    a[k] = u < 0 ? 0 : (u > 255 ? 255 : u);
+  }
+  __syncthreads();
+  for (int o = 0; o < ops.n; ++o) {
+    const int code = ops.code[o];
+    const float* p = ops.p[o];
+    if (code == AA_INVERT || code == AA_POSTERIZE || code == AA_SOLARIZE) {
+      const int mask = (int)p[0];
+      for (int k = tid; k < tot; k += blockDim.x) {
+        const int v = a[k];
+        a[k] = code == AA_INVERT ? 255 - v
+               : code == AA_POSTERIZE ? (v & mask)
+                                      : ((float)v >= p[0] ? 255 - v : v);
+      }
+    } else if (code >= AA_BLEND_ZERO && code <= AA_BLEND_BLUR) {
+      const float c1 = p[0], c2 = p[1];
+      float mean = 0.f;
+      if (code == AA_BLEND_MEAN) {
+        if (tid == 0) red[8] = 0;
+        __syncthreads();
+        int s = 0;
+        for (int k = tid; k < HW; k += blockDim.x) s += gray_u8(a[k], a[HW + k], a[2 * HW + k]);
+        atomicAdd(&red[8], s);
+        __syncthreads();
+        mean = (float)red[8] / (float)HW;  // exact integer sum, one rounding
+      }
+      if (code == AA_BLEND_BLUR && (H <= 2 || W <= 2)) continue;  // adjust_sharpness: identity
+      for (int k = tid; k < tot; k += blockDim.x) {
+        const int c = k / HW, pix = k - c * HW, i = pix / W, j = pix - i * W;
+        float other = 0.f;
+        if (code == AA_BLEND_GRAY) {
+          other = (float)gray_u8(a[pix], a[HW + pix], a[2 * HW + pix]);
+        } else if (code == AA_BLEND_MEAN) {
+          other = mean;
+        } else if (code == AA_BLEND_BLUR) {
+          if (i == 0 || j == 0 || i == H - 1 || j == W - 1) {
+            other = (float)a[k];
+          } else {
+            const float w1 = p[2], w5 = p[3];  // f32 1/13 and 5/13
+            float s = 0.f;
+            for (int di = -1; di <= 1; ++di)
+              for (int dj = -1; dj <= 1; ++dj)
+                s = __fadd_rn(s, __fmul_rn((float)a[k + di * W + dj], (di | dj) ? w1 : w5));
+            other = rintf(s);  // _cast_squeeze_out: round, then uint8
+          }
+        }
+        b[k] = trunc_u8(__fadd_rn(__fmul_rn(c1, (float)a[k]), __fmul_rn(c2, other)));
+      }
+      __syncthreads();
+      int* t = a; a = b; b = t;
+    } else if (code == AA_AUTOCONTRAST) {
+      if (tid < 4) { red[tid] = 255; red[4 + tid] = 0; }
+      __syncthreads();
+      for (int k = tid; k < tot; k += blockDim.x) {
+        const int c = k / HW;
+        atomicMin(&red[c], a[k]);
+        atomicMax(&red[4 + c], a[k]);
+      }
+      __syncthreads();
+      for (int k = tid; k < tot; k += blockDim.x) {
+        const int c = k / HW;
+        float mn = (float)red[c];
+        // `bound / (max - min)` with a Python-int numerator is Tensor.__rtruediv__:
+        // reciprocal(max - min) * 255, two roundings
+        float sc = __fmul_rn(__frcp_rn((float)red[4 + c] - mn), 255.0f);
+        if (!isfinite(sc)) { mn = 0.f; sc = 1.0f; }
+        a[k] = trunc_u8(__fmul_rn((float)a[k] - mn, sc));
+      }
+    } else if (code == AA_EQUALIZE) {
+      for (int k = tid; k < C * 256; k += blockDim.x) hist[k] = 0;
+      __syncthreads();
+      for (int k = tid; k < tot; k += blockDim.x) atomicAdd(&hist[(k / HW) * 256 + a[k]], 1);
+      __syncthreads();
+      if (tid < C) {
+        int* h = hist + tid * 256;
+        int last = 255;
+        while (last > 0 && h[last] == 0) --last;  // the last non-zero bin
+        int sum = 0;
+        for (int k = 0; k < last; ++k) sum += h[k];
+        const int step = sum / 255;
+        if (step == 0) {
+          for (int k = 0; k < 256; ++k) h[k] = k;  // unchanged channel
+        } else {
+          int cum = 0, prev = 0;
+          for (int k = 0; k < 256; ++k) {
+            cum += h[k];
+            const int v = (cum + step / 2) / step;  // lut before the shift
+            h[k] = prev;                            // pad [1, 0], drop the last
+            prev = v > 255 ? 255 : v;
+          }
+        }
+      }
+      __syncthreads();
+      for (int k = tid; k < tot; k += blockDim.x) a[k] = hist[(k / HW) * 256 + a[k]];
+    } else if (code == AA_AFFINE) {
+      for (int k = tid; k < tot; k += blockDim.x) {
+        const int c = k / HW, pix = k - c * HW, i = pix / W, j = pix - i * W;
+        const float xb = (float)j - 0.5f * (float)W + 0.5f, yb = (float)i - 0.5f * (float)H + 0.5f;
+        const float gx = __fadd_rn(__fadd_rn(__fmul_rn(xb, p[0]), __fmul_rn(yb, p[1])), p[2]);
+        const float gy = __fadd_rn(__fadd_rn(__fmul_rn(xb, p[3]), __fmul_rn(yb, p[4])), p[5]);
+        const float ix = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gx, 1.f), (float)W), 1.f), 2.f);
+        const float iy = __fdiv_rn(__fsub_rn(__fmul_rn(__fadd_rn(gy, 1.f), (float)H), 1.f), 2.f);
+        const int sx = (int)rintf(ix), sy = (int)rintf(iy);
+        b[k] = (sx >= 0 && sx < W && sy >= 0 && sy < H) ? a[c * HW + sy * W + sx] : 0;
+      }
+      __syncthreads();
+      int* t = a; a = b; b = t;
+    }
+    __syncthreads();
+  }
+  float* dst = out + (long)blockIdx.x * tot;
+  for (int k = tid; k < tot; k += blockDim.x) dst[k] = (float)a[k] / 255.0f;  // .float() / 255
+}
+
+}  // namespace
+
+extern "C" {
+
+int lc_autoaugment(hipStream_t st, int n, int C, int H, int W, const float* x, float* out,
+                   int n_ops, const int* codes, const float* params) {
+  LC_CHECK_ARG(n > 0 && C >= 1 && C <= 4 && H > 0 && W > 0 && C * H * W <= 12288);
+  LC_CHECK_ARG(n_ops >= 0 && n_ops <= 2 && x != nullptr && out != nullptr);
+  LC_CHECK_ARG(n_ops == 0 || (codes != nullptr && params != nullptr));
+  AugOps ops{};
+  ops.n = n_ops;
+  for (int o = 0; o < n_ops; ++o) {
+    LC_CHECK_ARG(codes[o] >= AA_INVERT && codes[o] <= AA_AFFINE);
+    LC_CHECK_ARG(!(codes[o] == AA_BLEND_GRAY || codes[o] == AA_BLEND_MEAN) || C == 3);
+    ops.code[o] = codes[o];
+    for (int k = 0; k < 6; ++k) ops.p[o][k] = params[o * 6 + k];
+  }
+  const size_t shm = (size_t)(2 * C * H * W + 4 * 256 + 16) * sizeof(int);
+  hipLaunchKernelGGL(autoaug_kernel, dim3(n), dim3(256), shm, st, C, H, W, x, out, ops);
+  LC_LAUNCH_RET();
+}
+
+}  // extern "C"

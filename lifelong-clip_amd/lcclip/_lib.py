@@ -38,6 +38,7 @@ SIGNATURES = {
     "lc_attn_bwd": [P, c_int, c_int, c_int, P, c_long, P, P, c_long, P, P, c_long, c_int],
     "lc_train_transform": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, P,
                            P, c_int, c_int, c_int, P],
+    "lc_autoaugment": [P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
     "lc_cast_bf16": [P, c_long, P, P],
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_cast_weights_bf16": [P, c_int, P, P, P, P, P],

@@ -483,14 +483,17 @@ def online_loop(task_batches, images, labels, class_tokens, p, cfg, method="adap
 
 
 # ----------------------------------------------------------------------------- train transform
-def train_transform(x, inp_size, padding, crop_i, crop_j, flip, mean, std, quantize=True):
+def train_transform(x, inp_size, padding, crop_i, crop_j, flip, mean, std, quantize=True,
+                    aug_ops=()):
     """methods/_trainer.py:212-242 on a batch tensor (torchvision tensor semantics: one parameter
-    draw per call, shared by the batch): the autoaug branch's uint8 round trip (:216, :229; the
-    AutoAugment op between them is NOT restated), Resize((S, S)) — torchvision's F.resize is
-    F.interpolate(bilinear, align_corners=False) (antialias is inert when upsampling) —,
-    RandomCrop(S, padding) = zero F.pad then the [i:i+S, j:j+S] window, hflip, Normalize
-    ((x - mean) / std)."""
-    if quantize:
+    draw per call, shared by the batch): the autoaug branch's uint8 round trip (:216, :229) with
+    the drawn AutoAugment ops between (aug_ops, see ``autoaugment``), Resize((S, S)) —
+    torchvision's F.resize is F.interpolate(bilinear, align_corners=False) (antialias is inert
+    when upsampling) —, RandomCrop(S, padding) = zero F.pad then the [i:i+S, j:j+S] window,
+    hflip, Normalize ((x - mean) / std)."""
+    if aug_ops:
+        x = autoaugment(x, aug_ops)
+    elif quantize:
         x = (x * 255).to(torch.uint8).to(torch.float32) / 255
     x = F.interpolate(x, size=(inp_size, inp_size), mode="bilinear", align_corners=False)
     x = F.pad(x, (padding, padding, padding, padding), value=0.0)
@@ -500,6 +503,141 @@ def train_transform(x, inp_size, padding, crop_i, crop_j, flip, mean, std, quant
     m = torch.tensor(mean, dtype=x.dtype).view(1, -1, 1, 1)
     s = torch.tensor(std, dtype=x.dtype).view(1, -1, 1, 1)
     return (x - m) / s
+
+
+# AutoAugment ops (torchvision 0.16.2 transforms/autoaugment.py _apply_op over
+# transforms/_functional_tensor.py, restated; torchvision is not installed here, so parity with
+# torchvision itself is unpinned). Images are uint8-valued int64 tensors [n, C, H, W]; every f32
+# expression is evaluated op by op in torch's order so the MI355X kernel (transform.hip
+# autoaug_kernel) can match bit for bit. Where torchvision evaluates with a bmm / conv2d whose
+# summation order is library-defined (the affine grid, the sharpness blur), the order fixed
+# here is left-to-right.
+def _f32(v):
+    return torch.tensor(v, dtype=torch.float32)
+
+
+def _aa_blend(img, other, ratio):
+    """_blend: (ratio * img + (1 - ratio) * other).clamp(0, 255).to(uint8)."""
+    r1, r2 = _f32(ratio), _f32(1.0 - ratio)
+    return (r1 * img.float() + r2 * other).clamp(0, 255).to(torch.uint8).long()
+
+
+def _aa_gray(img):
+    """rgb_to_grayscale on uint8: (0.2989 r + 0.587 g + 0.114 b).to(uint8)."""
+    r, g, b = img[:, 0].float(), img[:, 1].float(), img[:, 2].float()
+    return (_f32(0.2989) * r + _f32(0.587) * g + _f32(0.114) * b).to(torch.uint8).long()
+
+
+def _aa_affine_matrix(center, angle, translate, scale, shear):
+    """_get_inverse_affine_matrix (doubles)."""
+    rot, sx, sy = math.radians(angle), math.radians(shear[0]), math.radians(shear[1])
+    cx, cy = center
+    tx, ty = translate
+    a = math.cos(rot - sy) / math.cos(sy)
+    b = -math.cos(rot - sy) * math.tan(sx) / math.cos(sy) - math.sin(rot)
+    c = math.sin(rot - sy) / math.cos(sy)
+    d = -math.sin(rot - sy) * math.tan(sx) / math.cos(sy) + math.cos(rot)
+    m = [v / scale for v in (d, -b, 0.0, -c, a, 0.0)]
+    m[2] += m[0] * (-cx - tx) + m[1] * (-cy - ty) + cx
+    m[5] += m[3] * (-cx - tx) + m[4] * (-cy - ty) + cy
+    return m
+
+
+def _aa_affine(img, m):
+    """F_t.affine / F_t.rotate with NEAREST and no fill: _gen_affine_grid + grid_sample
+    (align_corners=False, zeros padding) + round to uint8."""
+    n, C, H, W = img.shape
+    t = torch.tensor(m, dtype=torch.float32)
+    hw, hh = _f32(0.5 * W), _f32(0.5 * H)
+    r = [t[0] / hw, t[1] / hw, t[2] / hw, t[3] / hh, t[4] / hh, t[5] / hh]
+    xs = torch.linspace(-W * 0.5 + 0.5, W * 0.5 + 0.5 - 1, W).view(1, W).expand(H, W)
+    ys = torch.linspace(-H * 0.5 + 0.5, H * 0.5 + 0.5 - 1, H).view(H, 1).expand(H, W)
+    gx = (xs * r[0] + ys * r[1]) + r[2]
+    gy = (xs * r[3] + ys * r[4]) + r[5]
+    ix = torch.round(((gx + 1) * W - 1) / 2).long()   # grid_sampler_unnormalize + nearbyint
+    iy = torch.round(((gy + 1) * H - 1) / 2).long()
+    ok = (ix >= 0) & (ix < W) & (iy >= 0) & (iy < H)
+    flat = (iy.clamp(0, H - 1) * W + ix.clamp(0, W - 1)).view(-1)
+    out = img.reshape(n, C, H * W)[:, :, flat].reshape(n, C, H, W)
+    return torch.where(ok, out, torch.zeros_like(out))
+
+
+def _aa_equalize_channel(ch):
+    hist = torch.bincount(ch.reshape(-1), minlength=256)
+    nz = hist[hist != 0]
+    step = int(nz[:-1].sum()) // 255
+    if step == 0:
+        return ch
+    lut = (torch.cumsum(hist, 0) + step // 2) // step
+    lut = torch.nn.functional.pad(lut, [1, 0])[:-1].clamp(0, 255)
+    return lut[ch]
+
+
+def aa_apply_op(img, op, mag):
+    """_apply_op(img, op_name, magnitude) for NEAREST interpolation and fill=None."""
+    n, C, H, W = img.shape
+    if op == "ShearX":
+        return _aa_affine(img, _aa_affine_matrix([-0.5 * W, -0.5 * H], 0.0, [0.0, 0.0], 1.0,
+                                                 [math.degrees(math.atan(mag)), 0.0]))
+    if op == "ShearY":
+        return _aa_affine(img, _aa_affine_matrix([-0.5 * W, -0.5 * H], 0.0, [0.0, 0.0], 1.0,
+                                                 [0.0, math.degrees(math.atan(mag))]))
+    if op == "TranslateX":
+        return _aa_affine(img, _aa_affine_matrix([0.0, 0.0], 0.0, [float(int(mag)), 0.0], 1.0,
+                                                 [0.0, 0.0]))
+    if op == "TranslateY":
+        return _aa_affine(img, _aa_affine_matrix([0.0, 0.0], 0.0, [0.0, float(int(mag))], 1.0,
+                                                 [0.0, 0.0]))
+    if op == "Rotate":
+        return _aa_affine(img, _aa_affine_matrix([0.0, 0.0], -mag, [0.0, 0.0], 1.0, [0.0, 0.0]))
+    if op == "Brightness":
+        return _aa_blend(img, torch.zeros(()), 1.0 + mag)
+    if op == "Color":
+        return _aa_blend(img, _aa_gray(img).float().unsqueeze(1), 1.0 + mag)
+    if op == "Contrast":
+        mean = _aa_gray(img).float().mean(dim=(-2, -1), keepdim=True).unsqueeze(1)
+        return _aa_blend(img, mean, 1.0 + mag)
+    if op == "Sharpness":
+        if H <= 2 or W <= 2:
+            return img
+        k = torch.ones(3, 3)
+        k[1, 1] = 5.0
+        k = k / k.sum()
+        f = img.float()
+        s = torch.zeros(n, C, H - 2, W - 2)
+        for di in range(3):
+            for dj in range(3):
+                s = s + f[:, :, di:di + H - 2, dj:dj + W - 2] * k[di, dj]
+        blur = img.clone()
+        blur[:, :, 1:-1, 1:-1] = torch.round(s).long()
+        return _aa_blend(img, blur.float(), 1.0 + mag)
+    if op == "Posterize":
+        return img & ((-int(2 ** (8 - int(mag)))) & 0xFF)
+    if op == "Solarize":
+        return torch.where(img.float() >= _f32(mag), 255 - img, img)
+    if op == "AutoContrast":
+        mn = img.amin(dim=(-2, -1), keepdim=True).float()
+        mx = img.amax(dim=(-2, -1), keepdim=True).float()
+        scale = 255 / (mx - mn)
+        bad = ~torch.isfinite(scale)
+        mn = torch.where(bad, torch.zeros_like(mn), mn)
+        scale = torch.where(bad, torch.ones_like(scale), scale)
+        return ((img.float() - mn) * scale).clamp(0, 255).to(torch.uint8).long()
+    if op == "Equalize":
+        return torch.stack([torch.stack([_aa_equalize_channel(img[i, c]) for c in range(C)])
+                            for i in range(n)])
+    if op == "Invert":
+        return 255 - img
+    raise ValueError(op)
+
+
+def autoaugment(x, ops):
+    """x f32 [n, C, H, W] in [0, 1] -> (x*255).type(uint8) -> the active ops in order ->
+    .float() / 255 (methods/_trainer.py:216-229)."""
+    img = (x * 255).to(torch.uint8).long()
+    for op, mag in ops:
+        img = aa_apply_op(img, op, mag)
+    return img.to(torch.float32) / 255
 
 
 def patchify(img, patch):

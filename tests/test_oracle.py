@@ -231,3 +231,54 @@ def test_mvp_oracle_pins():
     cos = torch.nn.functional.cosine_similarity(q.unsqueeze(1), mv["key"], dim=-1)
     assert torch.equal(full[5].flatten(), cos.argmax(1))
     assert torch.allclose(full[4], (torch.sigmoid(mv["mask"][cos.argmax(1)]) * 2)[:, :2])
+
+
+# ----------------------------------------------------------------------------- AutoAugment
+def test_autoaugment_known_answers():
+    """oracle.autoaugment (torchvision 0.16 ops restated) on hand-checkable cases."""
+    from oracle import clip_oracle as o
+    v = torch.tensor([0, 7, 100, 128, 200, 255]).float().view(1, 1, 1, 6).expand(1, 3, 1, 6) / 255
+    u = lambda y: (y * 255).round().long()[0, 0, 0].tolist()  # noqa: E731
+    assert u(o.autoaugment(v, [("Posterize", 5)])) == [0, 0, 96, 128, 200, 248]
+    assert u(o.autoaugment(v, [("Solarize", 128.0)])) == [0, 7, 100, 127, 55, 0]
+    assert u(o.autoaugment(v, [("Invert", 0.0)])) == [255, 248, 155, 127, 55, 0]
+    assert u(o.autoaugment(v, [("Brightness", -0.5)])) == [0, 3, 50, 64, 100, 127]
+    # equalize: a flat histogram (every value 4 times in 32x32) maps to itself
+    flat = (torch.arange(1024) // 4).float().view(1, 1, 32, 32).expand(1, 3, 32, 32) / 255
+    assert torch.equal(o.autoaugment(flat, [("Equalize", 0.0)]), o.autoaugment(flat, []))
+    # autocontrast stretches [50, 150] to [0, 255]
+    ac = o.autoaugment(torch.tensor([50., 100., 150.]).view(1, 1, 1, 3).expand(1, 3, 1, 3) / 255,
+                       [("AutoContrast", 0.0)])
+    assert u(ac) == [0, 127, 255]
+    # translations move whole columns / rows by int(magnitude) with zero fill; rotate(0) = id
+    img = torch.rand(2, 3, 32, 32)
+    q = o.autoaugment(img, [])
+    tx = o.autoaugment(img, [("TranslateX", 5.9)])
+    assert torch.equal(tx[..., 5:], q[..., :-5]) and (tx[..., :5] == 0).all()
+    ty = o.autoaugment(img, [("TranslateY", -3.2)])
+    assert torch.equal(ty[..., :-3, :], q[..., 3:, :]) and (ty[..., -3:, :] == 0).all()
+    assert torch.equal(o.autoaugment(img, [("Rotate", 0.0)]), q)
+    assert torch.equal(o.autoaugment(img, [("ShearX", 0.0)]), q)
+
+
+def test_autoaugment_draw_sequence():
+    """TrainTransform.draw consumes the generator in torchvision's order: AutoAugment.get_params
+    (randint(25), rand(2), randint(2, (2,))), then RandomCrop (randint x2), then the flip."""
+    from lcclip.transforms import AUTOAUG_POLICIES, TrainTransform, augmentation_space
+    tf = TrainTransform.for_dataset("cifar100", generator=torch.Generator().manual_seed(5))
+    ops, i, j, flip = tf.draw(32, 32)
+    g = torch.Generator().manual_seed(5)
+    tid = int(torch.randint(25, (1,), generator=g))
+    probs = torch.rand((2,), generator=g)
+    signs = torch.randint(2, (2,), generator=g)
+    want = []
+    space = augmentation_space(10, 32, 32)
+    for k, (op, p, mid) in enumerate(AUTOAUG_POLICIES["cifar10"][tid]):
+        if probs[k] <= p:
+            mags, signed = space[op]
+            m = float(mags[mid]) if mid is not None else 0.0
+            want.append((op, -m if signed and signs[k] == 0 else m))
+    assert ops == want
+    assert (i, j) == (int(torch.randint(0, 9, (1,), generator=g)),
+                      int(torch.randint(0, 9, (1,), generator=g)))
+    assert flip == bool(torch.rand(1, generator=g) < 0.5)
