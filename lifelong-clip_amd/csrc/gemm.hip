@@ -584,22 +584,24 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 // k-tile), barrier, MFMA part (16 bf16 16x16x32 or 8 scaled 16x16x128 MFMAs = 256 cycles),
 // barrier. Group 1 runs one barrier behind group 0, so on every SIMD one wave's MFMA part
 // overlaps the other's LOAD part.
-// DMA quarters (16 KiB, 2 global_load_lds per thread) in issue order: phase 0 of k-tile t: B rows
-// 128..255 of t+1; phase 1: A rows 0..127 of t+1 (+ the scale piece of t+1); phase 2: A rows
-// 128..255 of t+1; phase 3: B rows 0..127 of t+2. Hazards (barriers numbered by interval; G0's
-// LOAD(P) is interval 2P, G1's 2P+1): WAR — the first DMA into a buffer (B-lo of t+2, phase 3 of
-// t) follows the last read of B(t) (G1's phase-1 LOAD, retired in its phase-1 MFMA) by one
-// interval, A-top(t+2) / A-bot(t+2) follow the last A reads of t by >= 5. RAW — before G0 reads
-// k-tile t+1 (phase 0: A-top, B, scales) every wave has retired B-lo, B-hi, A-top(t+1): G0 at the
-// end of its phase-3 MFMA, G1 at the end of its phase-3 LOAD (each leaves A-bot(t+1) and
-// B-lo(t+2) in flight: vmcnt(4)); before G1 reads it (A-bot too) G0 retires A-bot(t+1) at the
-// end of its next LOAD (B-lo, B-hi of t+2 in flight) and G1 at the end of its phase-3 MFMA
-// (B-lo(t+2) in flight).
+// DMA quarters (16 KiB, 2 global_load_lds per thread), issued well ahead of their use: phase 0
+// of k-tile t: A rows 0..127 of t+1 (+ the scale piece of t+1); phase 1: A rows 128..255 of
+// t+1; phase 3: B rows 0..255 of t+2 (two quarters). Hazards (barriers numbered by interval;
+// G0's LOAD(P) is interval 2P, G1's 2P+1): WAR — B(t) is last read by G1's phase-1 LOAD,
+// retired in its phase-1 MFMA, 2 intervals before the first B(t+2) DMA; A(t-1) / scales(t-1)
+// are last read in phase 2 of t-1, >= 3 intervals before A(t+1) is issued. RAW — before G0
+// reads k-tile t+1 (phase 0: A rows 0..127, B, scales) every wave has retired them: G0 at the
+// end of its phase-3 MFMA, G1 at the end of its phase-3 LOAD (both leave A rows 128..255 of t+1
+// and B of t+2 in flight: vmcnt(6)); before G1 reads A rows 128..255 of t+1, G0 retires them at
+// the end of its next phase-0 LOAD (B(t+2), A rows 0..127 (t+2) in flight) and G1 at the end of
+// its phase-3 MFMA (B(t+2) in flight). So a quarter has 5-8 intervals to land.
 // A lane (g = lane >> 4) reads 16-B chunks g and g + 4 of a 128-B row in both forms: the bf16
 // operand's k-steps 0 and 1, and for fp8 exactly the bytes v_mfma_scale_f32_16x16x128_f8f6f4
 // takes from lane group g (k 16g..16g+15 in bytes 0-15, 64+16g.. in bytes 16-31; measured with
 // tools/dbg_fp8.py: hardware scale block b = k / 32 takes lane group b's scale byte, so each
 // lane passes the scale of block g). Conflict-free under the row XOR swizzle chunk ^ ((row >> 1) & 7).
+constexpr int TRACE_STAMPS_LOOP_END = 638;
+
 template <int EPI, bool FP8>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
@@ -613,7 +615,14 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   constexpr int BUF = TILE_A + TILE_B + SCALES;
   constexpr int SWM = 7;
   constexpr int KT = FP8 ? 128 : 64;  // k per k-tile
+#ifdef LC_GEMM_TRACE
+  // s_memtime stamps of waves 0 and 4 kept in LDS (global stores would break the counted
+  // vmcnt waits), copied out at the end: [group][640]
+  constexpr int TRACE_N = 640;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 2 * TRACE_N * 8];
+#else
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -649,6 +658,9 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   // DMA quarter `kind` of k-tile t: 0 = B rows 0..127, 1 = B rows 128..255, 2 = A rows 0..127
   // (+ scales), 3 = A rows 128..255
   auto dma = [&](int t, int kind) {
+#ifdef G8_NODMA  // diagnostic builds only: main-loop DMA off (results wrong)
+    if (t > 0) return;
+#endif
     char* buf = smem + (t & 1) * BUF;
     const bool isA = kind >= 2;
     const int half = kind & 1;
@@ -656,14 +668,15 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     const long ld = isA ? lda : ldb;
     const int rows_valid = isA ? M : N;
     const int r0 = isA ? m0 : n0;
-    char* dst = buf + (isA ? 0 : TILE_A) + half * (128 * 128);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = half * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+      const int row0 = half * 128 + (wave * 2 + i) * 8;  // one KiB, lane-linear in LDS
+      const int row = row0 + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & SWM);
       int gr = r0 + row;
       gr = gr < rows_valid ? gr : rows_valid - 1;  // tail rows computed, never stored
-      glds16(g + (long)gr * ld + (long)t * 128 + c * 16, dst + (wave * 2 + i) * 1024);
+      glds16(g + (long)gr * ld + (long)t * 128 + c * 16,
+             buf + (isA ? 0 : TILE_A) + row0 * 128);
     }
     if constexpr (FP8) {
       if (kind == 2) {
@@ -706,6 +719,9 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     return *reinterpret_cast<const uint8_t*>(p + g);
   };
   auto load_a = [&](const char* buf, int qm) {
+#ifdef G8_NOREAD  // diagnostic builds only: fragment reads off after the first k-tile
+    if (buf != smem) return;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ro = (qm * 64 + i * 16) * 128;
@@ -715,6 +731,9 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     }
   };
   auto load_b = [&](const char* buf, int qn) {
+#ifdef G8_NOREAD
+    if (buf != smem) return;
+#endif
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int ro = (qn * 32 + j * 16) * 128;
@@ -755,61 +774,99 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     pin(qm, qn);
   };
   const bool g0 = wr == 0;
+#ifdef LC_GEMM_TRACE
+  const int trace_wg = ep.dbg ? (int)(ep.dbg[0] >> 32) : -1;  // workgroup to trace (host-set)
+  const bool diag = ep.dbg != nullptr && (int)blockIdx.x == trace_wg && (wave & 3) == 0;
+  unsigned long long* tr = reinterpret_cast<unsigned long long*>(smem + 2 * BUF) + wr * TRACE_N;
+  auto stamp = [&](int idx) {
+    if (diag && idx < TRACE_N) {
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      if (lane == 0) tr[idx] = tt;
+    }
+  };
+#else
+  auto stamp = [](int) {};
+#endif
+  stamp(0);
 
-  // prologue: k-tile 0 whole, B rows 0..127 of k-tile 1; everything landed
+  // prologue: k-tile 0 whole, then B rows 0..255 of k-tile 1 (in flight across the barrier)
   dma(0, 0);
   dma(0, 1);
   dma(0, 2);
   dma(0, 3);
-  if (nt > 1) dma(1, 0);
-  wait_vmcnt<0>();
+  if (nt > 1) {
+    dma(1, 0);
+    dma(1, 1);
+    wait_vmcnt<4>();
+  } else {
+    wait_vmcnt<0>();
+  }
   __builtin_amdgcn_s_barrier();
   if (!g0) __builtin_amdgcn_s_barrier();  // group 1 one barrier behind
+  stamp(1);
 
+  constexpr int S = FP8 ? 1 : 0;  // scale glds riding with the A rows 0..127 quarter
   for (int t = 0; t < nt; ++t) {
     const char* buf = smem + (t & 1) * BUF;
     const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
-    // ---- phase 0: quadrant (0,0)
+    const int sb = 2 + t * 12;  // stamps of this k-tile: per phase [MFMA start, MFMA end, next start]
+    // ---- phase 0: quadrant (0,0); DMA A rows 0..127 (+ scales) of t+1
     load_a(buf, 0);
     load_b(buf, 0);
-    if (n1) dma(t + 1, 1);
-    if (g0) {  // A rows 128..255 of k-tile t retired (group 1 reads them next interval)
-      if (n1) wait_vmcnt<4>();
+    if (n1) dma(t + 1, 2);
+    if (g0) {  // A rows 128..255 of k-tile t retired (group 1 reads them next interval); B
+               // (t+1) and A rows 0..127 (t+1) may stay in flight
+      if (n1) wait_vmcnt<6 + S>();
       else wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    stamp(sb + 0);
     mma(0, 0);
+    stamp(sb + 1);
     __builtin_amdgcn_s_barrier();
-    // ---- phase 1: quadrant (0,1)
+    stamp(sb + 2);
+    // ---- phase 1: quadrant (0,1); DMA A rows 128..255 of t+1
     load_b(buf, 1);
-    if (n1) dma(t + 1, 2);
-    __builtin_amdgcn_s_barrier();
-    mma(0, 1);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase 2: quadrant (1,0)
-    load_a(buf, 1);
     if (n1) dma(t + 1, 3);
     __builtin_amdgcn_s_barrier();
-    mma(1, 0);
+    stamp(sb + 3);
+    mma(0, 1);
+    stamp(sb + 4);
     __builtin_amdgcn_s_barrier();
-    // ---- phase 3: quadrant (1,1), no reads
-    if (n2) dma(t + 2, 0);
+    stamp(sb + 5);
+    // ---- phase 2: quadrant (1,0), no DMA
+    load_a(buf, 1);
+    __builtin_amdgcn_s_barrier();
+    stamp(sb + 6);
+    mma(1, 0);
+    stamp(sb + 7);
+    __builtin_amdgcn_s_barrier();
+    stamp(sb + 8);
+    // ---- phase 3: quadrant (1,1), no reads; DMA B of t+2 (B(t) was last read in phase 1)
+    if (n2) {
+      dma(t + 2, 0);
+      dma(t + 2, 1);
+    }
     if (!g0) {  // B and A rows 0..127 (+ scales) of k-tile t+1 retired
-      if (n2) wait_vmcnt<4>();
+      if (n2) wait_vmcnt<6>();
       else if (n1) wait_vmcnt<2>();
     }
     __builtin_amdgcn_s_barrier();
+    stamp(sb + 9);
     mma(1, 1);
+    stamp(sb + 10);
     if (g0) {
-      if (n2) wait_vmcnt<4>();
+      if (n2) wait_vmcnt<6>();
       else if (n1) wait_vmcnt<2>();
     } else {  // A rows 128..255 of k-tile t+1 retired
-      if (n2) wait_vmcnt<2>();
+      if (n2) wait_vmcnt<4>();
       else wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+    stamp(sb + 11);
   }
   if (g0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
+  stamp(TRACE_STAMPS_LOOP_END);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   if (split >= 0) {
     const int tail = bid - sk.dp_tiles;
@@ -858,6 +915,12 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   }
   store_tile<BM, BN, WM, WN, EPI>(acc, smem, 2 * BUF, m0, n0, M, bias, alpha, out0, ldo0, out1,
                                   ldo1, aux, ldaux, ep);
+#ifdef LC_GEMM_TRACE
+  stamp(TRACE_N - 1);
+  __syncthreads();
+  if (diag)
+    for (int k = lane; k < TRACE_N; k += 64) ep.dbg[1 + wr * TRACE_N + k] = tr[k];
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
