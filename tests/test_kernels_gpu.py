@@ -281,7 +281,8 @@ def ref_attention(q, k, v, causal):
 
 @pytest.mark.parametrize("n,L,H,causal", [(3, 17, 2, False), (4, 77, 8, True), (2, 197, 12, False),
                                           (5, 32, 1, True), (2, 200, 2, False), (3, 224, 2, False),
-                                          (2, 256, 2, True), (1, 250, 3, False)])
+                                          (2, 256, 2, True), (1, 250, 3, False),
+                                          (2, 213, 3, True), (1, 193, 2, False)])
 def test_attention_fwd_bwd(ops, dev, n, L, H, causal):
     torch.manual_seed(3)
     D = H * 64

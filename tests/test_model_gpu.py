@@ -7,10 +7,10 @@ Tolerances (stated here):
       features rel-norm 5e-3 (what remains is accumulation order and bf16 rounding-boundary
       flips, e.g. of LoRA-merged weights);
   forward vs plain fp32 oracle: probs abs 1e-2, features rel-norm 2e-2 (the bf16 budget);
-  logits: max |dlogit| / exp(logit_scale) (= cosine-similarity error) < 1e-3 vs the
-      bf16-rounding oracle, < 2e-3 vs fp32;
-  PEFT gradients vs fp32 oracle: rel-norm 6e-2 per tensor (bf16 activations/gradients through
-      the frozen backbone);
+  logits: dlogit / exp(logit_scale) (cosine units, tests/parity.py): RMS < 1e-3 (north star)
+      and max < 2e-3 vs fp32, max < 8e-4 vs the bf16-rounding oracle;
+  PEFT gradients vs fp32 oracle: rel-norm 4e-2 per tensor (bf16 activations/gradients through
+      the frozen backbone; measured max 3.0e-2);
   AdamW: the HIP optimizer applied to the oracle's gradients reproduces the oracle's updated
       parameters to 1e-6 abs; the update from the HIP gradients agrees in sign with the
       oracle's on >= 90% of elements (Adam's first step is ~sign(g), so near-zero gradient
@@ -22,6 +22,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from parity import GRAD_REL, check_logits, logit_metrics
 
 from oracle import clip_oracle as o
 
@@ -78,7 +79,7 @@ def test_golden_trainer_step(golden, dev, method):
            loss_abs=eloss, grad_rel_max=max(grel.values()) if grel else None)
     assert e16 < 4e-3 and e32 < 1e-2 and eloss < 1e-2
     for name, r in grel.items():
-        assert r < 6e-2, (name, r)
+        assert r < GRAD_REL, (name, r)
     if not grel:
         return
     # (a) optimizer semantics: HIP AdamW on the oracle's gradients == oracle's new params
@@ -163,19 +164,71 @@ def test_vit_b16_full_shapes_vs_oracle(dev, method):
         probs, fi, ft = w(img.to(dev), tok.to(dev))
     ls = math.exp(math.log(1 / 0.07))
     lg = ls * fi.cpu() @ ft.cpu().t()
-    cos16 = ((lg - ls * i16 @ t16.t()).abs().max() / ls).item()
-    cos32 = ((lg - ls * i32 @ t32.t()).abs().max() / ls).item()
     m = dict(probs_abs_vs_bf16=(probs.cpu() - p16).abs().max().item(),
              probs_abs_vs_fp32=(probs.cpu() - p32).abs().max().item(),
              img_rel_vs_bf16=rel(fi, i16), txt_rel_vs_bf16=rel(ft, t16),
              img_rel_vs_fp32=rel(fi, i32), txt_rel_vs_fp32=rel(ft, t32),
-             cos_err_vs_bf16=cos16, cos_err_vs_fp32=cos32)
+             **logit_metrics(lg, ls * i32 @ t32.t(), ls * i16 @ t16.t(), ls))
     record(test="vit_b16_full_shapes", method=method, **m)
     assert m["probs_abs_vs_bf16"] < 4e-3 and m["probs_abs_vs_fp32"] < 1e-2
     assert m["img_rel_vs_bf16"] < 5e-3 and m["txt_rel_vs_bf16"] < 5e-3
     assert m["img_rel_vs_fp32"] < 2e-2 and m["txt_rel_vs_fp32"] < 2e-2
-    # logits (north-star target 1e-3): error in cosine units, i.e. |dlogit| / exp(logit_scale)
-    assert cos16 < 1e-3 and cos32 < 2e-3
+    check_logits(m)  # north star: logits within 1e-3 (cosine units, RMS)
+
+
+def _step_vs_oracle(dev, method, B, C, seed, tag):
+    """One fused trainer fwd + CE-on-probs + bwd at ViT-B/16 shapes vs the oracle's train_step
+    on the same weights: probs, loss, logits (tests/parity.py bounds) and every PEFT gradient.
+    Gradients, per tensor, vs the fp32 oracle and vs the bf16-rounding oracle: rel-norm <
+    GRAD_REL, or — where bf16 rounding itself moves that tensor's gradient further — within
+    1.25x + 1e-2 of the bf16-rounding oracle's own distance from fp32. That happens on the adapter
+    down-projections at large C: with near-uniform probabilities over 100 classes the loss
+    gradient is small and the per-row terms of dW_down = sum_rows dpre z^T mostly cancel, so any
+    bf16 evaluation (the oracle's included: up to 25 % from fp32 at C = 100, 22 % at C = 16 for
+    some seeds) lands far from fp32 on them while the well-conditioned tensors agree to ~3e-2."""
+    from lcclip import OnlineTrainer
+    cfg = o.VIT_B16
+    sd = o.synthetic_state_dict(cfg, method, "both", seed=seed)
+    img = o.synthetic_images(B, 224, seed=seed + 1)
+    tok = o.synthetic_tokens(C, 77, seed=seed + 2)
+    y = torch.arange(B) % C
+    loss32, p32, i32, t32, g32, _ = o.train_step(img, tok, y, sd, cfg, method, "both")
+    g16 = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16)[4]
+    w = make_wrapper(sd, method, "both", dev)
+    with torch.no_grad():
+        _, fi, ft = w(img.to(dev), tok.to(dev))
+    tr = OnlineTrainer(w)
+    loss, probs = tr.forward_backward(img.to(dev), y.to(dev), tok.to(dev))
+    torch.cuda.synchronize()
+    ls = math.exp(sd["logit_scale"].item())
+    named = dict(w.model.named_parameters())
+    e32 = {n: rel(tr.grads[named[n]], g) for n, g in g32.items()}
+    e16 = {n: rel(tr.grads[named[n]], g16[n]) for n in g32}
+    eo = {n: rel(g16[n], g32[n]) for n in g32}
+    m = dict(probs_abs_vs_fp32=(probs.cpu() - p32).abs().max().item(),
+             loss_abs=abs(loss.item() - loss32.item()), grad_rel_max_vs_fp32=max(e32.values()),
+             grad_rel_max_vs_bf16=max(e16.values()), oracle_bf16_grad_rel_max=max(eo.values()),
+             n_grads=len(e32), **logit_metrics(ls * fi.cpu() @ ft.cpu().t(),
+                                                ls * i32 @ t32.t(), None, ls))
+    record(test=tag, method=method, B=B, C=C, **m)
+    assert m["probs_abs_vs_fp32"] < 1e-2 and m["loss_abs"] < 1e-2, m
+    check_logits(m)
+    for n in g32:
+        bound = max(GRAD_REL, 1.25 * eo[n] + 1e-2)
+        assert e16[n] < bound and e32[n] < bound, (n, e16[n], e32[n], eo[n])
+    return m
+
+
+def test_lora_config1_shape_step_vs_oracle(dev):
+    """BASELINE config 1's shape: LoRA on both towers, B = 16 images, C = 16 prompts."""
+    m = _step_vs_oracle(dev, "lora", 16, 16, 61, "lora_b16_c16_step")
+    assert m["n_grads"] > 0
+
+
+def test_adapter_c100_step_vs_oracle(dev):
+    """Config 2's C = 100 stress through the model: 100 class prompts in the text tower (one
+    launch of 100 x 77 rows per GEMM), the B x 100 head, CE on probs, adapter gradients."""
+    _step_vs_oracle(dev, "adapter", 4, 100, 71, "adapter_c100_step")
 
 
 def test_vit_b16_batch256_properties(dev):
