@@ -393,9 +393,13 @@ struct BwdLds {
   static constexpr int BYTES = ND_OFF + LP * 4;
 };
 
-template <int NQB>
+// Persistent: a workgroup walks (sequence, head) items blockIdx.x, + gridDim.x, ...; the next
+// item's Q / dO / O / lse rows and K / V fragments are loaded into registers while the current
+// one computes (rows after the current item's LDS image is written, K / V after its phase 1), so
+// the item's HBM traffic (~230 KB at L = 197) overlaps the MFMA / exp work of the previous one.
+template <int NQB, bool PERSIST = (NQB >= 5)>
 __global__ void __launch_bounds__(64 * NQB)
-attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
+attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
                    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
                    const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
                    float scale) {
@@ -411,39 +415,71 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, t = lane & 15;
-  const int nh = blockIdx.x, n = nh / H, h = nh % H;
-  const long base = (long)n * L;
   const float c = scale * LOG2E;
+  int item = blockIdx.x;
+  if (item >= n_items) return;
 
-  // staging: all 16-B loads of Q, dO and O issued before the first LDS write; D = rowsum(dO*O)
-  // from the same chunks (8 lanes per row, reduced with xor-shuffles)
+  // staging: 16-B chunks of Q, dO and O rows (8 lanes per row); D = rowsum(dO*O) from the same
+  // chunks (xor-shuffles) when they are written to LDS
   constexpr int IT = LP * 8 / NTH;  // = 4
   const int ch = tid & 7;
   uint4 qv[IT], dv[IT], ov[IT];
   float lv[IT];
+  // Q rows and lse (prefetched during phase 1), dO and O rows (during phase 2: registers). The
+  // per-lane row offsets are recomputed from an opaque copy of tid at every call: hoisted out of
+  // the item loop they would stay live through both phases (and spill).
+  auto lane_tid = [&]() {
+    int v = tid;
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto load_rows = [&](int it_) {
+    const int tv = lane_tid();
+    const bf16_t* qb = qkv + (long)(it_ / H) * L * ldq + (it_ % H) * 64 + (tv & 7) * 8;
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int r = (tid + i * NTH) >> 3;
-    const long off = h * 64 + ch * 8;
-    qv[i] = ld16_or_zero(qkv + (base + r) * ldq + off, r < L);
-    dv[i] = ld16_or_zero(dO + (base + r) * ldo + off, r < L);
-    ov[i] = ld16_or_zero(O + (base + r) * ldo + off, r < L);
-    lv[i] = (r < L) ? lse[(long)nh * L + r] : 1e30f;
-  }
+    for (int i = 0; i < IT; ++i) {
+      const int r = (tv + i * NTH) >> 3;
+      qv[i] = ld16_or_zero(qb + r * (int)ldq, r < L);
+      lv[i] = (r < L) ? lse[(long)it_ * L + r] : 1e30f;
+    }
+  };
+  auto load_o = [&](int it_) {
+    const int tv = lane_tid();
+    const long rb = (long)(it_ / H) * L * ldo + (it_ % H) * 64 + (tv & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int r = (tv + i * NTH) >> 3;
+      dv[i] = ld16_or_zero(dO + rb + r * (int)ldo, r < L);
+      ov[i] = ld16_or_zero(O + rb + r * (int)ldo, r < L);
+    }
+  };
   // own key block: K / V rows kb + kt2*16 + t, as B-operand fragments
   const int kb = 32 * w;
   bf16x8 kf[2][2], vf[2][2];
+  auto load_kv = [&](int it_) {
+    const int tv = lane_tid() & 63;
+    const bf16_t* kb_ = qkv + (long)(it_ / H) * L * ldq + (it_ % H) * 64 + D + (tv >> 4) * 8;
 #pragma unroll
-  for (int kt2 = 0; kt2 < 2; ++kt2) {
-    const int key = kb + kt2 * 16 + t;
+    for (int kt2 = 0; kt2 < 2; ++kt2) {
+      const int key = kb + kt2 * 16 + (tv & 15);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16_t* src = qkv + (base + key) * ldq + h * 64 + s * 32 + g * 8;
-      uint4 ku = ld16_or_zero(src + D, key < L), vu = ld16_or_zero(src + 2 * D, key < L);
-      kf[kt2][s] = *reinterpret_cast<bf16x8*>(&ku);
-      vf[kt2][s] = *reinterpret_cast<bf16x8*>(&vu);
+      for (int s = 0; s < 2; ++s) {
+        const bf16_t* src = kb_ + key * (int)ldq + s * 32;
+        uint4 ku = ld16_or_zero(src, key < L), vu = ld16_or_zero(src + D, key < L);
+        kf[kt2][s] = *reinterpret_cast<bf16x8*>(&ku);
+        vf[kt2][s] = *reinterpret_cast<bf16x8*>(&vu);
+      }
     }
-  }
+  };
+  load_rows(item);
+  load_o(item);
+  load_kv(item);
+
+#pragma unroll 1
+  for (; item < n_items; item += gridDim.x) {
+  const int next = item + gridDim.x;
+  const int h = item % H;
+  const long base = (long)(item / H) * L;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int r = (tid + i * NTH) >> 3;
@@ -464,6 +500,7 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
     }
   }
   __syncthreads();
+  if (PERSIST && next < n_items) load_rows(next);  // in flight through phases 1 and 2
 
   const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
   const int tr0 = tr_off(t, g, 0), tr1 = tr_off(t, g, 1), tr2 = tr_off(t, g, 2), tr3 = tr_off(t, g, 3);
@@ -560,6 +597,10 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
       const int key = kb + kt2 * 16 + t;
       *reinterpret_cast<bf16x8*>(Ks + key * 128 + swz(key, s * 4 + g) * 16) = kf[kt2][s];
     }
+  if (PERSIST && next < n_items) {  // kf / vf, phase-1 accumulators dead until the next item
+    load_o(next);
+    load_kv(next);
+  }
   __syncthreads();
 
   // phase 2: dQ^T[d][q] = sum_key K^T[d][key] dS^T[key][q] for queries qb..qb+31 (k order:
@@ -603,6 +644,9 @@ attn_bwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
             uint2{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale)};
       }
     }
+  }
+  if constexpr (!PERSIST) break;  // one item per workgroup (short sequences: many workgroups)
+  __syncthreads();  // phase 2 done with Ks / dS^T before the next item's LDS image
   }
 }
 
@@ -736,6 +780,23 @@ attn_bwd_q_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   }
 }
 
+// workgroups of a persistent launch: as many as fit on the chip at once (LDS-limited) when there
+// are many items per workgroup (L = 197: 3072 items, 12 per workgroup), else one per item
+int persistent_grid(int items, int lds_bytes) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per_cu = (160 * 1024) / lds_bytes;
+  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+  const int g = cus * per_cu;
+  // a few items per workgroup would leave a ragged last round: one item each (no pipelining)
+  return items < 4 * g ? items : g;
+}
+
 }  // namespace
 
 extern "C" {
@@ -798,9 +859,11 @@ int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
                          (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
                          lse, (bf16_t*)dqkv, lddq, causal, scale);                             \
     else                                                                                       \
-      hipLaunchKernelGGL(attn_bwd_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,               \
-                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
-                         lse, (bf16_t*)dqkv, lddq, causal, scale);                             \
+      hipLaunchKernelGGL(attn_bwd_kernel<Q>,                                                   \
+                         dim3(Q >= 5 ? persistent_grid(n_seq * H, BwdLds<Q>::BYTES) : n_seq * H),\
+                         dim3(64 * Q), 0, st, n_seq * H, L, H, D, (const bf16_t*)qkv, ldq,      \
+                         (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, (bf16_t*)dqkv, lddq,    \
+                         causal, scale);                                                       \
     break;
     LC_AB(1) LC_AB(2) LC_AB(3) LC_AB(4) LC_AB(5) LC_AB(6) LC_AB(7)
 #undef LC_AB
