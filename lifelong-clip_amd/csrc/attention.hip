@@ -38,8 +38,16 @@ LC_DEV bool masked(int key, int q, int L, int causal) {
   return (key >= L) | ((causal != 0) & (key > q));
 }
 
-// 128-B-row images: 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7)
-LC_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// 128-B-row images: 16-B chunk c of row r lives at chunk c ^ m(r), m(r) = x ^ ((x << 1) & 7) with
+// x = (r >> 1) & 7: conflict-free both for row reads (ds_read_b128: lane t reads row t) and for the
+// transposed reads (ds_read_b64_tr_b16: 8 rows x 32 B per 32 lanes; the plain x ^ chunk mask put
+// rows r and r + 2 on the same banks there, 2-way) — checked exhaustively for every lane group.
+// Period 16 rows, so lane offsets stay valid for any 16-row-aligned block.
+LC_DEV int swz_mask(int row) {
+  const int x = (row >> 1) & 7;
+  return x ^ ((x << 1) & 7);
+}
+LC_DEV int swz(int row, int chunk) { return chunk ^ swz_mask(row); }
 
 LC_DEV bf16x8 lds16(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 LC_DEV bf16x4 lds_tr(const char* p) {
@@ -63,7 +71,7 @@ LC_DEV uint4 ld16_or_zero(const bf16_t* p, bool ok) {
 //   tr_off(t, g, dt): transposed read of rows 4g + (t>>2) (+16 for the upper half), columns
 //                     dt*16 + (t&3)*4 .. +3 — the V^T / K^T / Q^T / dO^T fragment layout whose
 //                     k order matches a bf16x8 packed from two 16-row accumulator tiles.
-LC_DEV int row_off(int t, int g, int s) { return t * 128 + (((s * 4 + g) ^ ((t >> 1) & 7)) * 16); }
+LC_DEV int row_off(int t, int g, int s) { return t * 128 + swz(t, s * 4 + g) * 16; }
 LC_DEV int tr_off(int t, int g, int dt) {
   const int row = 4 * g + (t >> 2);
   const int col = dt * 16 + (t & 3) * 4;
