@@ -45,6 +45,24 @@ constexpr int BK = 64;
 
 LC_DEV int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// Tile raster of the 256x256 GEMMs: linear tile index -> (row panel tm, column tile tn), in groups
+// of gm row panels walked column-major inside the group, so that the workgroups one XCD runs at
+// once (a contiguous index range, see the XCD remap) share a few B column slices across gm
+// A panels instead of all of B across ~tiles/XCD / tiles_n panels (B = the weight, 4.7 MB at
+// N = 3072, K = 768, more than one XCD's 4 MB L2). gm <= 1: row-major.
+LC_DEV void tile_coords(int tile, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = tile / tiles_n;
+    tn = tile % tiles_n;
+    return;
+  }
+  const int per = gm * tiles_n;
+  const int grp = tile / per, idx = tile % per;
+  const int rows = min(gm, tiles_m - grp * gm);
+  tm = grp * gm + idx % rows;
+  tn = idx / rows;
+}
+
 template <int ROWS, int NW>
 LC_DEV void stage_tile(const bf16_t* __restrict__ g, long ld, int row0, int rows_valid, int k0,
                        char* lds, int tid) {
@@ -643,7 +661,8 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     tb = split * nt_all / sk.splits;
     te = (split + 1) * nt_all / sk.splits;
   }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  int tm, tn;
+  tile_coords(bid, (M + BM - 1) / BM, tiles_n, ep.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int nt = te - tb;
   const char* __restrict__ A = static_cast<const char*>(Av) + (long)tb * 128;
@@ -959,7 +978,8 @@ gemm_w4_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
   }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  int tm, tn;
+  tile_coords(bid, tiles_m, tiles_n, ep.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int ns = K / 32;
 
@@ -1506,9 +1526,24 @@ SplitK plan_split(int tiles, int units, int min_units, void* ws, long ws_bytes) 
   return sk;
 }
 
+// row panels per tile-raster group of the 256x256 GEMMs (tile_coords; env LC_GEMM_GM forces one).
+// Measured (tools/gpu_gm.sh, M = 50 432): groups of 8 panels help the wide-N shapes (QKV fwd
+// N = 2304: 181 -> 174 us, c_fc fwd N = 3072: 311 -> 303-307 us, c_proj dX -1 %) and cost the
+// N = 768 ones 1-3 % (3 column tiles: the row-major raster already shares B)
+int group_m(int N) {
+  static const int forced = [] {
+    const char* e = getenv("LC_GEMM_GM");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced) return forced;
+  return N >= 2304 ? 8 : 1;
+}
+
 int launch_w4(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
-              void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep_in) {
+  EpiParams ep = ep_in;
+  ep.group_m = group_m(N);
   const int tiles = ((M + 255) / 256) * (N / 256);
   dim3 grid(tiles), block(256);
 #define LC_W4_CASE(E)                                                                          \
@@ -1566,8 +1601,10 @@ int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
 template <bool FP8>
 int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long lda,
               const void* B, long ldb, const float* bias, float alpha, void* o0, long l0,
-              void* o1, long l1, const void* aux, long la, const EpiParams& ep, void* ws,
+              void* o1, long l1, const void* aux, long la, const EpiParams& ep_in, void* ws,
               long ws_bytes, const Fp8Scales& sc) {
+  EpiParams ep = ep_in;
+  ep.group_m = group_m(N);
   const int tiles = ((M + 255) / 256) * (N / 256);
   const int units = K / (FP8 ? 128 : 64);
   const SplitK sk = plan_split(tiles, units, 8, ws, ws_bytes);
