@@ -27,14 +27,18 @@ import torch.distributed as dist
 
 
 class DataParallel:
-    """Rank bookkeeping + the three exchanges. world == 1 makes every call a no-op."""
+    """Rank bookkeeping + the three exchanges. world == 1 makes every call a no-op, unless the
+    collectives are forced (env LCCLIP_DP_FORCE=1 with an initialised process group: the same
+    calls run on a one-rank group, so the RCCL path executes on a one-GPU box)."""
 
     def __init__(self, group=None, enabled=None):
+        import os
         on = dist.is_available() and dist.is_initialized()
         self.enabled = on if enabled is None else (enabled and on)
         self.group = group
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.rank = dist.get_rank(group) if self.enabled else 0
+        self.active = self.world > 1 or (self.enabled and os.environ.get("LCCLIP_DP_FORCE") == "1")
         self._works = []
 
     # ---------------------------------------------------------------- prompt sharding
@@ -54,7 +58,7 @@ class DataParallel:
 
     def gather_rows(self, rows, C: int):
         """All-gather the per-rank [per, E] feature slices into [C, E] (padding dropped)."""
-        if self.world == 1:
+        if not self.active:
             return rows[:C]
         parts = [torch.empty_like(rows) for _ in range(self.world)]
         dist.all_gather(parts, rows.contiguous(), group=self.group)
@@ -62,18 +66,18 @@ class DataParallel:
 
     def sum_async(self, t):
         """Asynchronous in-place SUM all-reduce; returns a handle with .wait() (or None)."""
-        if self.world == 1:
+        if not self.active:
             return None
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     # ---------------------------------------------------------------- gradient buckets
     def launch_bucket(self, flat, lo: int, hi: int):
-        if self.world > 1 and hi > lo:
+        if self.active and hi > lo:
             self._works.append(self.sum_async(flat[lo:hi]))
 
     def finish_buckets(self, flat):
         """Wait for every bucket and turn the sums into means."""
-        if self.world == 1:
+        if not self.active:
             return
         for w in self._works:
             w.wait()

@@ -52,7 +52,7 @@ class OnlineTrainer:
         self.txt = self.clip.text_tower
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.dp = DataParallel(process_group, distributed)
-        self.distributed = self.dp.world > 1
+        self.distributed = self.dp.active
         self.shard_text = shard_text and self.distributed
         self.bucket_layers = max(1, int(bucket_layers))
         img_params = self.img.stack.trainable_params()
@@ -146,20 +146,17 @@ class OnlineTrainer:
         d_tp = torch.zeros(per * dp.world if self.shard_text else C, E, dtype=F32, device=dev)
         ops.head_feat_grad(dlog, C, 1, txt_n, img_n, ni, self.logit_scale, d_i)
         train_txt = ct is not None and bool(self.txt.stack.trainable_params())
-        # dL/dT (a sum over the batch per prompt) is only needed by the text backward: unless it
-        # is all-reduced first, it is computed on the text stream, off the image chain
-        w_dt = None
-        if self.shard_text and train_txt:
-            ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
-            w_dt = dp.sum_async(d_tp)
+        # dL/dT (a sum over the batch per prompt) is only needed by the text backward: it is
+        # computed on the text stream, off the image chain, and (sharded text) all-reduced from
+        # there, so RCCL's stream follows the text stream and only the text backward waits for it
         if train_txt:
             if side is not None:
                 side.wait_stream(main)
             with torch.cuda.stream(side) if side is not None else _nullctx():
+                ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
+                w_dt = dp.sum_async(d_tp) if self.shard_text else None
                 if w_dt is not None:
-                    w_dt.wait()  # makes the text stream wait for the dL/dT all-reduce
-                else:
-                    ops.head_feat_grad(dlog, 1, C, img_n, txt_n, nt, self.logit_scale, d_tp[:C])
+                    w_dt.wait()  # the current (text) stream waits for the dL/dT all-reduce
                 self.txt.backward(ct, d_tp[lo:hi].contiguous(), self.grads)
         if self.img.stack.trainable_params():
             self.img.backward(ci, d_i, self.grads, on_layer=self._img_bucket_hook(),
@@ -213,10 +210,18 @@ class OnlineTrainer:
 
         def hook(li):
             if li % self.bucket_layers == 0:
-                self.img.stack.sync_grads()  # the bucket's gradients are complete
                 lo_r = self.img_ranges[li][0]
                 hi_r = self.img_ranges[state["hi"] - 1][1]
-                self.dp.launch_bucket(self.flat_g, lo_r, hi_r)
+                gs = getattr(self.img.stack, "_gs", None)
+                if gs is None:
+                    self.dp.launch_bucket(self.flat_g, lo_r, hi_r)
+                else:
+                    # the bucket's gradients come from both streams: the gradient stream waits
+                    # for the main one (never the reverse: the main chain keeps running) and the
+                    # all-reduce is issued from it, so RCCL's stream follows both
+                    gs.wait_stream(torch.cuda.current_stream(gs.device))
+                    with torch.cuda.stream(gs):
+                        self.dp.launch_bucket(self.flat_g, lo_r, hi_r)
                 state["hi"] = li
         return hook
 

@@ -1,7 +1,10 @@
 """The trainer's data-parallel path on the GPU: two ranks share cuda:0 over gloo (the box has one
 GPU; RCCL needs one GPU per rank), each takes one image of the golden batch and its slice of the
 prompts; after the bucketed exchange both ranks must hold the gradients the single-process
-trainer computes on the whole batch (up to the changed fp32 / bf16 summation order)."""
+trainer computes on the whole batch (up to the changed fp32 / bf16 summation order). The RCCL
+(backend "nccl") path itself runs at world size 1: the same protocol (text-row all-gather,
+dL/dT all-reduce, bucketed async PEFT-gradient all-reduces on the collective stream) must give
+the single-process gradients bit for bit."""
 import os
 import socket
 import sys
@@ -88,3 +91,40 @@ def test_trainer_dp_matches_single_process(dev, method):
         if r.norm() > 0:
             assert ((g[off:off + k] - r).norm() / r.norm()).item() < 5e-2
         off += k
+
+
+def _worker_nccl(rank, world, port, tmpdir, method):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LCCLIP_DP_FORCE"] = "1"  # run the collectives on the one-rank group
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    assert dist.get_backend() == "nccl"
+    tr, img, tok, y = _trainer(method, True)
+    assert tr.dp.world == 1 and tr.distributed and tr.shard_text
+    for _ in range(2):  # two steps: buckets, graph-free async path, optimizer in between
+        tr.forward_backward(img, y, tok)
+        tr.all_reduce_grads()
+        torch.cuda.synchronize()
+        torch.save(tr.flat_g.cpu(), os.path.join(tmpdir, f"g{_}.pt"))
+        tr.optimizer_step()
+    torch.save(tr.flat_p.cpu(), os.path.join(tmpdir, "p.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("method", ["lora", "adapter"])
+def test_trainer_dp_rccl_world1(dev, method):
+    tr, img, tok, y = _trainer(method, False)
+    refs = []
+    for _ in range(2):
+        tr.forward_backward(img, y, tok)
+        torch.cuda.synchronize()
+        refs.append(tr.flat_g.cpu())
+        tr.optimizer_step()
+    ref_p = tr.flat_p.cpu()
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker_nccl, args=(1, _free_port(), tmp, method), nprocs=1, join=True)
+        gs = [torch.load(os.path.join(tmp, f"g{i}.pt"), weights_only=True) for i in range(2)]
+        p = torch.load(os.path.join(tmp, "p.pt"), weights_only=True)
+    for g, r in zip(gs, refs):
+        assert torch.equal(g, r)
+    assert torch.equal(p, ref_p)
