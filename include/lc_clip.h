@@ -225,6 +225,13 @@ int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg,
 int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
                      const void* z, long ldz, const void* dpre, float scale, float* dWu,
                      float* dbu, float* dWd, float* dbd);
+/* The same with a two-stage reduction: every walker's partial goes to ws (after its first
+ * LC_SPLITK_TICKET_BYTES, left untouched: the split-K workspace of the launch stream can be
+ * passed) and a second launch sums them into the outputs, instead of f32 atomics. Falls back to
+ * the atomics when ws is NULL or smaller than LC_SPLITK_TICKET_BYTES + 2 x 256 x 8384 x 4 B. */
+int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                        const void* h, const void* z, long ldz, const void* dpre, float scale,
+                        float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes);
 
 /* *flag |= any(!isfinite(g))  (GradScaler's inf check, _trainer.py:163, adapter_clip.py:94). */
 int lc_check_finite(hipStream_t stream, long n, const float* g, int* flag);

@@ -794,9 +794,10 @@ int persistent_grid(int items, int lds_bytes) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (cus <= 0) cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
   }
   int per_cu = (160 * 1024) / lds_bytes;
   per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);

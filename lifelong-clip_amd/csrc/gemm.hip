@@ -1271,7 +1271,12 @@ struct TnProb {
   float* cs_s;        // += cs_s_scale * sum_m S[m][j]   (j < ns), or nullptr
   float cs_s_scale;
   int M, n_chunks, n_tiles, wgs;  // row-block walkers per panel, W panels, workgroups
+  float* part;        // two-stage mode: one partial slot per workgroup (tn_reduce_kernel sums
+                      // them into C / the column sums); nullptr: f32 atomics into C
 };
+
+// partial slot of one walker: P [128 panel columns][64], then 128 W column sums, 64 S column sums
+constexpr int TN_SLOT = 128 * 64 + 128 + 64;
 
 constexpr int TNW_STAGES = 5;
 constexpr int TNW_SLOT = 64 * 256 + 64 * 128;  // W panel 64 x 128 bf16 + S 64 x 64 bf16
@@ -1315,7 +1320,12 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
   // block-cyclic rows: walker cidx takes 64-row blocks cidx, cidx + n_chunks, ... so that the
   // workgroups of the grid sweep one contiguous band of rows together (DRAM-page locality)
   const int nblk = (p.M + 63) / 64;
-  if (cidx >= nblk) return;
+  float* slot = p.part ? p.part + (long)(tile * p.n_chunks + cidx) * TN_SLOT : nullptr;
+  if (cidx >= nblk) {  // no rows (plan_tn never makes such walkers): an empty partial
+    if (slot)
+      for (int e = tid; e < TN_SLOT; e += 512) slot[e] = 0.f;
+    return;
+  }
   const int nsteps = (nblk - 1 - cidx) / p.n_chunks + 1;
   auto blk_row = [&](int s) { return (cidx + s * p.n_chunks) * 64; };
   const int nw_pad = (p.Nw + 63) & ~63;
@@ -1407,6 +1417,21 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
     }
   }
   // lane holds P[n = tile*128 + 32wn + 16i + 4g + r][j = 32wsv + 16jj + t]
+  if (slot) {  // two-stage: plain stores of the whole partial (masking happens in the reduce)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nl = wn * 32 + i * 16 + g * 4 + r;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) slot[nl * 64 + wsv * 32 + jj * 16 + t] = acc[i][jj][r];
+        if (wsv == 0 && t == 0) slot[8192 + nl] = do_csw ? csw[i][r] : 0.f;
+      }
+    if (wn == 0 && g == 0)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) slot[8192 + 128 + wsv * 32 + jj * 16 + t] = do_css ? css[jj][0] : 0.f;
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1429,6 +1454,44 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wsv * 32 + jj * 16 + t;
       if (j < p.ns) atomicAdd(p.cs_s + j, css[jj][0] * p.cs_s_scale);
+    }
+  }
+}
+
+// Second stage of the two-stage PEFT weight-gradient reduction: one thread per output (P
+// element, W column sum or S column sum) of both problems sums the walkers' partial slots and
+// adds the result into C / the column sums (each output owned by one thread: no atomics).
+__global__ void __launch_bounds__(256)
+tn_reduce_kernel(TnProb p0, TnProb p1) {
+  const int np0 = p0.Nw * 64 + p0.Nw + 64;
+  const int np1 = p1.part ? p1.Nw * 64 + p1.Nw + 64 : 0;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < np0 + np1; e += gridDim.x * 256) {
+    const bool second = e >= np0;
+    const TnProb& p = second ? p1 : p0;
+    const int k = second ? e - np0 : e;
+    if (k < p.Nw * 64) {  // P[n][j]
+      const int n = k / 64, j = k % 64;
+      if (j >= p.ns) continue;
+      const int tile = n / 128, nl = n % 128;
+      const float* src = p.part + (long)tile * p.n_chunks * TN_SLOT + nl * 64 + j;
+      float v = 0.f;
+      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      float* dst = p.trans ? p.C + (long)j * p.ldc + n : p.C + (long)n * p.ldc + j;
+      *dst += v * p.alpha;
+    } else if (k < p.Nw * 64 + p.Nw) {  // column sums of W
+      if (!p.cs_w) continue;
+      const int n = k - p.Nw * 64, tile = n / 128, nl = n % 128;
+      const float* src = p.part + (long)tile * p.n_chunks * TN_SLOT + 8192 + nl;
+      float v = 0.f;
+      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      p.cs_w[n] += v * p.cs_w_scale;
+    } else {  // column sums of S (tile 0's walkers carry them)
+      const int j = k - p.Nw * 64 - p.Nw;
+      if (!p.cs_s || j >= p.ns) continue;
+      const float* src = p.part + 8192 + 128 + j;
+      float v = 0.f;
+      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      p.cs_s[j] += v * p.cs_s_scale;
     }
   }
 }
@@ -1814,6 +1877,13 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
 int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
                      const void* z, long ldz, const void* dpre, float scale, float* dWu,
                      float* dbu, float* dWd, float* dbd) {
+  return lc_adapter_wgrad_ws(stream, M, D, gout, ldg, h, z, ldz, dpre, scale, dWu, dbu, dWd, dbd,
+                             nullptr, 0);
+}
+
+int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                        const void* h, const void* z, long ldz, const void* dpre, float scale,
+                        float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes) {
   LC_CHECK_ARG(M > 0 && D > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0 && ldg >= D &&
                ldz >= D);
   LC_CHECK_ARG(dWu != nullptr && dWd != nullptr);
@@ -1852,7 +1922,19 @@ int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ld
   plan_tn(down, 2 * down.n_tiles);
   static const bool skip = getenv("LC_DIAG_SKIP_WGRAD") != nullptr;  // timing knockout only
   if (skip) return LC_OK;
+  // two-stage reduction when the workspace holds every walker's partial (after the split-K
+  // ticket region, which must stay zero): plain stores + one small summing launch instead of
+  // 8192 f32 atomics per walker
+  const long need = (long)(up.wgs + down.wgs) * TN_SLOT * 4;
+  if (ws != nullptr && ws_bytes >= LC_SPLITK_TICKET_BYTES + need) {
+    up.part = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
+    down.part = up.part + (long)up.wgs * TN_SLOT;
+  }
   hipLaunchKernelGGL(gemm_tn_wide_kernel, dim3(up.wgs + down.wgs), dim3(512), 0, stream, up, down);
+  if (up.part) {
+    const int outs = 2 * (D * 64 + D + 64);
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3((outs + 255) / 256), dim3(256), 0, stream, up, down);
+  }
   LC_LAUNCH_RET();
 }
 

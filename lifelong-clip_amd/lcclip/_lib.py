@@ -47,6 +47,8 @@ SIGNATURES = {
                        P, c_long, P],
     "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long],
     "lc_adapter_wgrad": [P, c_int, c_int, P, c_long, P, P, c_long, P, c_float, P, P, P, P],
+    "lc_adapter_wgrad_ws": [P, c_int, c_int, P, c_long, P, P, c_long, P, c_float, P, P, P, P, P,
+                            c_long],
     "lc_check_finite": [P, c_long, P, P],
     "lc_adamw": [P, c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, P, P],
     "lc_counter_add": [P, c_int, P, c_long],

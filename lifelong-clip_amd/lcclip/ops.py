@@ -285,8 +285,12 @@ def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
     for t in (dWu, dWd, dbu, dbd):
         if t is not None and (t.dtype != F32 or not t.is_contiguous()):
             raise ValueError("gradient buffers must be contiguous f32")
-    call("lc_adapter_wgrad", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
-         z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd))
+    # two-stage reduction through the launch stream's split-K workspace (partials after its
+    # ticket region; the stream orders every user of that buffer)
+    ws = splitk_workspace(torch.cuda.current_stream(gout.device))
+    call("lc_adapter_wgrad_ws", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
+         z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd), ptr(ws),
+         ws.numel())
 
 
 def check_finite(g, flag):

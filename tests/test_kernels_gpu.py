@@ -205,11 +205,18 @@ def test_adapter_wgrad(ops, dev, M, D):
     dbu = torch.full((D,), 2.0, device=dev)
     dWd = torch.full((64, D), 2.0, device=dev)
     dbd = torch.full((64,), 2.0, device=dev)
-    ops.adapter_wgrad(gout, h, z, dpre, 0.1, dWu, dbu, dWd, dbd)
+    ops.adapter_wgrad(gout, h, z, dpre, 0.1, dWu, dbu, dWd, dbd)  # two-stage (workspace)
     assert rel(dWu - 2, 0.1 * gout.float().t() @ h.float()) < 1e-5
     assert rel(dbu - 2, 0.1 * gout.float().sum(0)) < 1e-5
     assert rel(dWd - 2, dpre.float().t() @ z.float()) < 1e-5
     assert rel(dbd - 2, dpre.float().sum(0)) < 1e-5
+    # the single-stage form (f32 atomics, no workspace) on the same inputs
+    from lcclip._lib import call, ptr, stream_of
+    out = [torch.full_like(t, 2.0) for t in (dWu, dbu, dWd, dbd)]
+    call("lc_adapter_wgrad", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
+         z.stride(0), ptr(dpre), 0.1, *[ptr(t) for t in out])
+    for a, b in zip(out, (dWu, dbu, dWd, dbd)):
+        assert rel(a - 2, b - 2) < 1e-6
 
 
 def test_gemm_tn_masked_rank4(ops, dev):

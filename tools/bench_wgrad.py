@@ -26,13 +26,24 @@ dbd = torch.zeros(64, device=dev)
 for _ in range(3):
     ops.adapter_wgrad(g, h, z, dp, 0.1, dWu, dbu, dWd, dbd)
 reps = 20
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(reps):
-    ops.adapter_wgrad(g, h, z, dp, 0.1, dWu, dbu, dWd, dbd)
-e1.record()
-torch.cuda.synchronize()
-us = e0.elapsed_time(e1) / reps * 1e3
+from lcclip._lib import call, ptr, stream_of  # noqa: E402
+
+
+def atomics():
+    call("lc_adapter_wgrad", stream_of(g), M, D, ptr(g), g.stride(0), ptr(h), ptr(z), z.stride(0),
+         ptr(dp), 0.1, ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd))
+
+
 nbytes = (g.numel() + z.numel() + h.numel() + dp.numel()) * 2
-print(f"walkers={os.environ.get('LC_TN_WALKERS', 'cu')} M={M}: {us:.1f} us  "
-      f"{nbytes / us / 1e3:.0f} GB/s", flush=True)
+for name, fn in (("two-stage", lambda: ops.adapter_wgrad(g, h, z, dp, 0.1, dWu, dbu, dWd, dbd)),
+                 ("atomics", atomics)):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    print(f"{name:9s} walkers={os.environ.get('LC_TN_WALKERS', 'cu')} M={M}: {us:.1f} us  "
+          f"{nbytes / us / 1e3:.0f} GB/s", flush=True)
