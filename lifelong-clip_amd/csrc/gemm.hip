@@ -1273,18 +1273,30 @@ struct TnProb {
   int M, n_chunks, n_tiles, wgs;  // row-block walkers per panel, W panels, workgroups
   float* part;        // two-stage mode: one partial slot per workgroup (tn_reduce_kernel sums
                       // them into C / the column sums); nullptr: f32 atomics into C
+  int pw;             // W panel width of the launch (128 or 256)
 };
 
-// partial slot of one walker: P [128 panel columns][64], then 128 W column sums, 64 S column sums
-constexpr int TN_SLOT = 128 * 64 + 128 + 64;
+// Geometry of the wide x skinny reduction for a W panel of PW columns (128 or 256; 256 halves
+// the re-reads of S, one per panel, for the adapter's D = 768: 3 panels instead of 6).
+template <int PW>
+struct TnGeom {
+  static constexpr int ROWB = PW * 2;              // W panel row bytes (256 / 512)
+  static constexpr int WB = 64 * ROWB;             // W bytes of one 64-row step
+  static constexpr int SLOT = WB + 64 * 128;       // + S 64 x 64 bf16
+  static constexpr int STAGES = (5 * 24576) / SLOT;  // 5 / 3 slots: 120 KiB of ring
+  static constexpr int WPW = WB / 1024 / 8;        // W 1-KiB pieces per wave per step (2 / 4)
+  static constexpr int LOADS = WPW + 1;            // glds per wave per step (+ one S piece)
+  static constexpr int TI = PW / 64;               // 16-column W blocks per wave (2 / 4)
+};
 
-constexpr int TNW_STAGES = 5;
-constexpr int TNW_SLOT = 64 * 256 + 64 * 128;  // W panel 64 x 128 bf16 + S 64 x 64 bf16
-constexpr int TNW_LOADS = (16 + 8) / 8;        // glds instructions per wave per slot
+// partial slot of one walker (two-stage mode): P [pw panel columns][64], pw W column sums,
+// 64 S column sums
+__host__ __device__ inline int tn_pslot(int pw) { return pw * 64 + pw + 64; }
 
 // LDS images are XOR-swizzled in 32-B units so that the 8 rows {0..3, 8..11} (+16) one
 // ds_read_b64_tr_b16 pass of 32 lanes touches land in 8 distinct 32-B bank groups.
-//   W rows (256 B = 8 units): unit u of row r at u ^ ((r & 3) | ((r >> 1) & 4))
+//   W rows (256 or 512 B): unit u of row r at u ^ ((r & 3) | ((r >> 1) & 4)) (low 3 bits: a
+//     row's bank offset only depends on u mod 8 for both widths)
 //   S rows (128 B = 4 units; two rows per 256-B bank span): unit u at u ^ (((r >> 1) & 1) | ((r >> 2) & 2))
 LC_DEV int swz_w(int r) { return (r & 3) | ((r >> 1) & 4); }
 LC_DEV int swz_s(int r) { return ((r >> 1) & 1) | ((r >> 2) & 2); }
@@ -1295,7 +1307,7 @@ template <int ROWB>
 LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
   auto addr = [&](int r) {
     const int byte = col * 2;  // within the row
-    const int u = (byte >> 5) ^ (ROWB == 256 ? swz_w(r) : swz_s(r));
+    const int u = (byte >> 5) ^ (ROWB >= 256 ? swz_w(r) : swz_s(r));
     return lds + r * ROWB + u * 32 + (byte & 31);
   };
   const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1305,10 +1317,15 @@ LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// 8 waves: wave w owns W columns 32 (w & 3) .. +31 and S columns 32 (w >> 2) .. +31 of the panel.
+// 8 waves: wave w owns W columns (PW/4) (w & 3) .. +PW/4 and S columns 32 (w >> 2) .. +31.
+template <int PW>
 __global__ void __launch_bounds__(512, 1)
 gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
-  __shared__ __attribute__((aligned(16))) char smem[TNW_STAGES * TNW_SLOT];
+  using Geo = TnGeom<PW>;
+  constexpr int STAGES = Geo::STAGES, SLOT = Geo::SLOT, LOADS = Geo::LOADS, TI = Geo::TI;
+  constexpr int ROWB = Geo::ROWB, LPRW = ROWB / 16, RPP = 64 / LPRW;  // lanes / rows per W piece
+  constexpr int PSLOT = PW * 64 + PW + 64;
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * SLOT];
   const bool second = (int)blockIdx.x >= p0.wgs;
   const TnProb& p = second ? p1 : p0;
   const int bid = second ? blockIdx.x - p0.wgs : blockIdx.x;
@@ -1320,10 +1337,10 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
   // block-cyclic rows: walker cidx takes 64-row blocks cidx, cidx + n_chunks, ... so that the
   // workgroups of the grid sweep one contiguous band of rows together (DRAM-page locality)
   const int nblk = (p.M + 63) / 64;
-  float* slot = p.part ? p.part + (long)(tile * p.n_chunks + cidx) * TN_SLOT : nullptr;
+  float* slot = p.part ? p.part + (long)(tile * p.n_chunks + cidx) * PSLOT : nullptr;
   if (cidx >= nblk) {  // no rows (plan_tn never makes such walkers): an empty partial
     if (slot)
-      for (int e = tid; e < TN_SLOT; e += 512) slot[e] = 0.f;
+      for (int e = tid; e < PSLOT; e += 512) slot[e] = 0.f;
     return;
   }
   const int nsteps = (nblk - 1 - cidx) / p.n_chunks + 1;
@@ -1334,19 +1351,19 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
 
   // DMA of step s into slot s % STAGES. A wave-instruction fills 1 KiB of LDS linearly; the
   // lane -> (row, unit) map inverts the swizzle (source chosen so that lane*16 is its slot).
-  //   W: 4 rows per piece, lane -> row lane >> 4, position 16-B chunk lane & 15
+  //   W: RPP rows per piece, lane -> row lane / LPRW, position 16-B chunk lane % LPRW
   //   S: 8 rows per piece, lane -> row lane >> 3, position chunk lane & 7
   auto dma = [&](int s) {
-    char* sl = smem + (s % TNW_STAGES) * TNW_SLOT;
+    char* sl = smem + (s % STAGES) * SLOT;
     const int r0 = blk_row(s);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = wave * 2 + i;  // 16 W pieces
-      const int lr = piece * 4 + (lane >> 4);
-      const int pc = lane & 15;
+    for (int i = 0; i < Geo::WPW; ++i) {
+      const int piece = wave * Geo::WPW + i;
+      const int lr = piece * RPP + lane / LPRW;
+      const int pc = lane % LPRW;
       const int c = (((pc >> 1) ^ swz_w(lr)) << 1) | (pc & 1);  // source 16-B chunk
       const int r = min(r0 + lr, p.M - 1);
-      int col = tile * 128 + c * 8;
+      int col = tile * PW + c * 8;
       col = col < nw_pad ? col : col - 64;  // past a 64-multiple Nw: re-read, masked at the store
       glds16(p.W + (long)r * p.ldw + col, sl + piece * 1024);
     }
@@ -1356,43 +1373,45 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
       const int pc = lane & 7;
       const int c = (((pc >> 1) ^ swz_s(lr)) << 1) | (pc & 1);
       const int r = min(r0 + lr, p.M - 1);
-      glds16(p.S + (long)r * p.lds + c * 8, sl + 64 * 256 + piece * 1024);
+      glds16(p.S + (long)r * p.lds + c * 8, sl + Geo::WB + piece * 1024);
     }
   };
 
-  f32x4 acc[2][2], csw[2], css[2];
+  f32x4 acc[TI][2], csw[TI], css[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    csw[i] = css[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < TI; ++i) {
+    csw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  css[0] = css[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const short one = (short)0x3F80;
 
 #pragma unroll
-  for (int s = 0; s < TNW_STAGES - 1; ++s)
+  for (int s = 0; s < STAGES - 1; ++s)
     if (s < nsteps) dma(s);
   for (int s = 0; s < nsteps; ++s) {
     // own DMA of step s landed (up to STAGES-2 later steps may stay in flight); after the
     // barrier every wave's has, and every wave is done reading slot (s-1) % STAGES, which the
     // DMA of step s + STAGES - 1 overwrites
-    const int ahead = min(nsteps - 1 - s, TNW_STAGES - 2);
-    if (ahead >= 3) wait_vmcnt<3 * TNW_LOADS>();
-    else if (ahead == 2) wait_vmcnt<2 * TNW_LOADS>();
-    else if (ahead == 1) wait_vmcnt<TNW_LOADS>();
+    const int ahead = min(nsteps - 1 - s, STAGES - 2);
+    if (STAGES > 4 && ahead >= 3) wait_vmcnt<3 * LOADS>();
+    else if (STAGES > 3 && ahead == 2) wait_vmcnt<2 * LOADS>();
+    else if (ahead >= 1) wait_vmcnt<LOADS>();
     else wait_vmcnt<0>();
     __syncthreads();
-    if (s + TNW_STAGES - 1 < nsteps) dma(s + TNW_STAGES - 1);
-    const char* sw = smem + (s % TNW_STAGES) * TNW_SLOT;
-    const char* ss = sw + 64 * 256;
+    if (s + STAGES - 1 < nsteps) dma(s + STAGES - 1);
+    const char* sw = smem + (s % STAGES) * SLOT;
+    const char* ss = sw + Geo::WB;
     const int valid = p.M - blk_row(s);  // rows of this block inside M (>= 64: all)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int row = ks * 32 + g * 8 + (t >> 2);
       const int kb = ks * 32 + g * 8;
-      bf16x8 fw[2], fs[2];
+      bf16x8 fw[TI], fs[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fw[i] = tr_frag<256>(sw, row, wn * 32 + i * 16 + (t & 3) * 4);
+      for (int i = 0; i < TI; ++i)
+        fw[i] = tr_frag<ROWB>(sw, row, wn * (PW / 4) + i * 16 + (t & 3) * 4);
 #pragma unroll
       for (int j = 0; j < 2; ++j) fs[j] = tr_frag<128>(ss, row, wsv * 32 + j * 16 + (t & 3) * 4);
       bf16x8 ones;
@@ -1405,7 +1424,7 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
           for (int e = 0; e < 8; ++e) fs[j][e] = (kb + e < valid) ? fs[j][e] : (short)0;
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < TI; ++i) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fw[i], fs[j], acc[i][j]);
         if (do_csw) csw[i] = mfma16(fw[i], ones, csw[i]);
@@ -1416,27 +1435,28 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
       }
     }
   }
-  // lane holds P[n = tile*128 + 32wn + 16i + 4g + r][j = 32wsv + 16jj + t]
+  // lane holds P[n = tile*PW + (PW/4) wn + 16i + 4g + r][j = 32wsv + 16jj + t]
   if (slot) {  // two-stage: plain stores of the whole partial (masking happens in the reduce)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int nl = wn * 32 + i * 16 + g * 4 + r;
+        const int nl = wn * (PW / 4) + i * 16 + g * 4 + r;
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) slot[nl * 64 + wsv * 32 + jj * 16 + t] = acc[i][jj][r];
-        if (wsv == 0 && t == 0) slot[8192 + nl] = do_csw ? csw[i][r] : 0.f;
+        if (wsv == 0 && t == 0) slot[PW * 64 + nl] = do_csw ? csw[i][r] : 0.f;
       }
     if (wn == 0 && g == 0)
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) slot[8192 + 128 + wsv * 32 + jj * 16 + t] = do_css ? css[jj][0] : 0.f;
+      for (int jj = 0; jj < 2; ++jj)
+        slot[PW * 64 + PW + wsv * 32 + jj * 16 + t] = do_css ? css[jj][0] : 0.f;
     return;
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int n = tile * 128 + wn * 32 + i * 16 + g * 4 + r;
+      const int n = tile * PW + wn * (PW / 4) + i * 16 + g * 4 + r;
       if (n >= p.Nw) continue;
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -1469,28 +1489,30 @@ tn_reduce_kernel(TnProb p0, TnProb p1) {
     const bool second = e >= np0;
     const TnProb& p = second ? p1 : p0;
     const int k = second ? e - np0 : e;
+    const int pw = p.pw;
+    const long ps = tn_pslot(pw);
     if (k < p.Nw * 64) {  // P[n][j]
       const int n = k / 64, j = k % 64;
       if (j >= p.ns) continue;
-      const int tile = n / 128, nl = n % 128;
-      const float* src = p.part + (long)tile * p.n_chunks * TN_SLOT + nl * 64 + j;
+      const int tile = n / pw, nl = n % pw;
+      const float* src = p.part + (long)tile * p.n_chunks * ps + nl * 64 + j;
       float v = 0.f;
-      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      for (int c = 0; c < p.n_chunks; ++c) v += src[c * ps];
       float* dst = p.trans ? p.C + (long)j * p.ldc + n : p.C + (long)n * p.ldc + j;
       *dst += v * p.alpha;
     } else if (k < p.Nw * 64 + p.Nw) {  // column sums of W
       if (!p.cs_w) continue;
-      const int n = k - p.Nw * 64, tile = n / 128, nl = n % 128;
-      const float* src = p.part + (long)tile * p.n_chunks * TN_SLOT + 8192 + nl;
+      const int n = k - p.Nw * 64, tile = n / pw, nl = n % pw;
+      const float* src = p.part + (long)tile * p.n_chunks * ps + pw * 64 + nl;
       float v = 0.f;
-      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      for (int c = 0; c < p.n_chunks; ++c) v += src[c * ps];
       p.cs_w[n] += v * p.cs_w_scale;
     } else {  // column sums of S (tile 0's walkers carry them)
       const int j = k - p.Nw * 64 - p.Nw;
       if (!p.cs_s || j >= p.ns) continue;
-      const float* src = p.part + 8192 + 128 + j;
+      const float* src = p.part + pw * 64 + pw + j;
       float v = 0.f;
-      for (int c = 0; c < p.n_chunks; ++c) v += src[(long)c * TN_SLOT];
+      for (int c = 0; c < p.n_chunks; ++c) v += src[c * ps];
       p.cs_s[j] += v * p.cs_s_scale;
     }
   }
@@ -1854,10 +1876,11 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
     p.cs_s = a_wide ? nullptr : colsum;
     p.cs_s_scale = colsum_scale;
     p.M = M;
+    p.pw = 128;
     p.n_tiles = (p.Nw + 127) / 128;
     plan_tn(p, p.n_tiles);
     TnProb none{};
-    hipLaunchKernelGGL(gemm_tn_wide_kernel, dim3(p.wgs), dim3(512), 0, stream, p, none);
+    hipLaunchKernelGGL(gemm_tn_wide_kernel<128>, dim3(p.wgs), dim3(512), 0, stream, p, none);
     LC_LAUNCH_RET();
   }
   const int tiles = ((N1 + 63) / 64) * ((N2 + 63) / 64);
@@ -1901,8 +1924,11 @@ int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long
   up.alpha = scale;
   up.cs_w = dbu;
   up.cs_w_scale = scale;
+  // 256-column W panels when D allows (half the re-reads of h / dpre, one per panel)
+  const int pw = D % 256 == 0 ? 256 : 128;
+  up.pw = pw;
   up.M = M;
-  up.n_tiles = (D + 127) / 128;
+  up.n_tiles = (D + pw - 1) / pw;
   // dWd[64][D] += dpre^T z = (z^T dpre)^T ; dbd += colsum(dpre)
   down.W = static_cast<const bf16_t*>(z);
   down.ldw = ldz;
@@ -1916,8 +1942,9 @@ int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long
   down.alpha = 1.0f;
   down.cs_s = dbd;
   down.cs_s_scale = 1.0f;
+  down.pw = pw;
   down.M = M;
-  down.n_tiles = (D + 127) / 128;
+  down.n_tiles = (D + pw - 1) / pw;
   plan_tn(up, 2 * up.n_tiles);
   plan_tn(down, 2 * down.n_tiles);
   static const bool skip = getenv("LC_DIAG_SKIP_WGRAD") != nullptr;  // timing knockout only
@@ -1925,12 +1952,17 @@ int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long
   // two-stage reduction when the workspace holds every walker's partial (after the split-K
   // ticket region, which must stay zero): plain stores + one small summing launch instead of
   // 8192 f32 atomics per walker
-  const long need = (long)(up.wgs + down.wgs) * TN_SLOT * 4;
+  const long need = (long)(up.wgs + down.wgs) * tn_pslot(pw) * 4;
   if (ws != nullptr && ws_bytes >= LC_SPLITK_TICKET_BYTES + need) {
     up.part = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
-    down.part = up.part + (long)up.wgs * TN_SLOT;
+    down.part = up.part + (long)up.wgs * tn_pslot(pw);
   }
-  hipLaunchKernelGGL(gemm_tn_wide_kernel, dim3(up.wgs + down.wgs), dim3(512), 0, stream, up, down);
+  if (pw == 256)
+    hipLaunchKernelGGL(gemm_tn_wide_kernel<256>, dim3(up.wgs + down.wgs), dim3(512), 0, stream, up,
+                       down);
+  else
+    hipLaunchKernelGGL(gemm_tn_wide_kernel<128>, dim3(up.wgs + down.wgs), dim3(512), 0, stream, up,
+                       down);
   if (up.part) {
     const int outs = 2 * (D * 64 + D + 64);
     hipLaunchKernelGGL(tn_reduce_kernel, dim3((outs + 255) / 256), dim3(256), 0, stream, up, down);

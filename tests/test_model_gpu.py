@@ -234,6 +234,12 @@ def test_lora_config1_shape_step_vs_oracle(dev):
     assert m["n_grads"] > 0
 
 
+def test_adapter_config2_b32_step_vs_oracle(dev):
+    """BASELINE config 2's method and prompt count (adapter both towers, C = 10) at B = 32: a
+    larger batch than the B = 2 forward cases, the full train step against the oracle."""
+    _step_vs_oracle(dev, "adapter", 32, 10, 81, "adapter_b32_c10_step")
+
+
 def test_adapter_c100_step_vs_oracle(dev):
     """Config 2's C = 100 stress through the model: 100 class prompts in the text tower (one
     launch of 100 x 77 rows per GEMM), the B x 100 head, CE on probs, adapter gradients."""
