@@ -1283,7 +1283,10 @@ struct TnGeom {
   static constexpr int ROWB = PW * 2;              // W panel row bytes (256 / 512)
   static constexpr int WB = 64 * ROWB;             // W bytes of one 64-row step
   static constexpr int SLOT = WB + 64 * 128;       // + S 64 x 64 bf16
-  static constexpr int STAGES = (5 * 24576) / SLOT;  // 5 / 3 slots: 120 KiB of ring
+#ifndef TNW256_STAGES
+#define TNW256_STAGES 3
+#endif
+  static constexpr int STAGES = PW == 256 ? TNW256_STAGES : 5;  // 120 KiB of ring (160 at 4)
   static constexpr int WPW = WB / 1024 / 8;        // W 1-KiB pieces per wave per step (2 / 4)
   static constexpr int LOADS = WPW + 1;            // glds per wave per step (+ one S piece)
   static constexpr int TI = PW / 64;               // 16-column W blocks per wave (2 / 4)

@@ -67,11 +67,14 @@ class LcError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH):
-    """Load liblcclip.so and declare every entry point. Raises if anything is missing."""
+def load(path: str = None):
+    """Load liblcclip.so and declare every entry point. Raises if anything is missing.
+    LCCLIP_LIB=<path> selects another build of the same library (A/B experiments)."""
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:
+        path = os.environ.get("LCCLIP_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise LcError(f"liblcclip.so not built at {path}; run `python __graft_entry__.py build` "
                       "(there is no CPU fallback)")
