@@ -106,6 +106,13 @@ int lc_gemm_set_debug(unsigned long long* p);
  * (models/clip/adapter.py:38-40, 59-62). */
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
                long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale);
+/* The same with a workspace (ws after its first LC_SPLITK_TICKET_BYTES, which stay untouched:
+ * the launch stream's split-K workspace can be passed): in the wide x skinny case with the wide
+ * side a multiple of 256 columns, 256-column panels and a two-stage reduction (partials to ws, a
+ * summing launch) replace the f32 atomics. Falls back to lc_gemm_tn's path otherwise. */
+int lc_gemm_tn_ws(hipStream_t stream, int M, int N1, int N2, const void* A, long lda,
+                  const void* B, long ldb, float alpha, float* C, long ldc, float* colsum,
+                  float colsum_scale, void* ws, long ws_bytes);
 
 /* LayerNorm over rows of width D (64 <= D <= 1024, D % 64 == 0), fp32 statistics, eps 1e-5.
  * y is bf16 (y_f32 = 0) or f32 (y_f32 = 1); row_idx (optional) gathers input rows.

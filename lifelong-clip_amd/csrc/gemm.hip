@@ -1755,8 +1755,21 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     // and the 128x128 kernel on N = K = 768 (858 vs ~780 TF); 128x128 at 2 workgroups/CU for
     // launches with fewer 256x256 tiles than CUs (text tower, MaPLe's 64-image batch at N =
     // 768: 150 tiles) — those would leave CUs idle
+    // Rounds of 256x256 tiles: a ragged last round costs a whole tile time unless split-K can
+    // spread it (K >= 1024: plan_split's 2 x 8 k-tiles) — measured at MaPLe's shapes
+    // (tools/gpu_tn.sh, M = 7700 text / 12 800 image): with ~1.1-1.5 rounds the 128x128 kernel
+    // wins (QKV fwd 39.7 vs 45.2 us, c_fc fwd 53.5 vs 59.1); with >= 2 full rounds, a tail over
+    // half a round or a splittable tail the 256x256 one does (every M = 50 432 shape). Below one
+    // round it still wins from half a round on when K is long (N = 768, K >= 2304 at 150 tiles:
+    // 65.6 vs 83.4 us for 128x128, 73.8 for 128x64); N = 768 otherwise: 128x64 tiles (K = 768:
+    // 24.3 vs 26.7 us; K = 3072 at 93 tiles: 46.5 vs 48.5).
+    const int t256 = ((M + 255) / 256) * (N / 256), cus = cu_count();
+    const int full = t256 / cus, rem = t256 % cus;
+    const bool tail_ok = full >= 2 || rem == 0 || 2 * rem >= cus || (2 * rem <= cus && K >= 1024);
     if (N % 128 != 0) tile = 4;
-    else if (M >= 4096 && N % 256 == 0 && ((M + 255) / 256) * (N / 256) >= cu_count()) tile = 8;
+    else if (M >= 4096 && N % 256 == 0 && t256 >= cus && tail_ok) tile = 8;
+    else if (M >= 4096 && N % 256 == 0 && 2 * t256 >= cus && K >= 2048) tile = 8;
+    else if (M >= 4096 && N <= 768) tile = 4;
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 289 vs 295 us (bench_gemm.py)
     if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048) tile = 7;
@@ -1855,6 +1868,13 @@ int lc_gemm_set_tile(int tile) {
 
 int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
                long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale) {
+  return lc_gemm_tn_ws(stream, M, N1, N2, A, lda, B, ldb, alpha, C, ldc, colsum, colsum_scale,
+                       nullptr, 0);
+}
+
+int lc_gemm_tn_ws(hipStream_t stream, int M, int N1, int N2, const void* A, long lda,
+                  const void* B, long ldb, float alpha, float* C, long ldc, float* colsum,
+                  float colsum_scale, void* ws, long ws_bytes) {
   LC_CHECK_ARG(M > 0 && N1 > 0 && N2 > 0);
   // operand rows are read in 64-column blocks: they must be readable up to the next multiple
   // of 64 (zero padding); outputs beyond N1 x N2 are masked
@@ -1879,11 +1899,23 @@ int lc_gemm_tn(hipStream_t stream, int M, int N1, int N2, const void* A, long ld
     p.cs_s = a_wide ? nullptr : colsum;
     p.cs_s_scale = colsum_scale;
     p.M = M;
-    p.pw = 128;
-    p.n_tiles = (p.Nw + 127) / 128;
+    // with a workspace: 256-column panels (half the re-reads of the skinny operand) and the
+    // two-stage reduction, when the wide side is a multiple of 256
+    const bool wide = ws != nullptr && p.Nw % 256 == 0;
+    p.pw = wide ? 256 : 128;
+    p.n_tiles = (p.Nw + p.pw - 1) / p.pw;
     plan_tn(p, p.n_tiles);
+    if (wide && ws_bytes >= LC_SPLITK_TICKET_BYTES + (long)p.wgs * tn_pslot(p.pw) * 4)
+      p.part = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
     TnProb none{};
-    hipLaunchKernelGGL(gemm_tn_wide_kernel<128>, dim3(p.wgs), dim3(512), 0, stream, p, none);
+    if (p.pw == 256)
+      hipLaunchKernelGGL(gemm_tn_wide_kernel<256>, dim3(p.wgs), dim3(512), 0, stream, p, none);
+    else
+      hipLaunchKernelGGL(gemm_tn_wide_kernel<128>, dim3(p.wgs), dim3(512), 0, stream, p, none);
+    if (p.part) {
+      const int outs = p.Nw * 64 + p.Nw + 64;
+      hipLaunchKernelGGL(tn_reduce_kernel, dim3((outs + 255) / 256), dim3(256), 0, stream, p, none);
+    }
     LC_LAUNCH_RET();
   }
   const int tiles = ((N1 + 63) / 64) * ((N2 + 63) / 64);

@@ -28,6 +28,8 @@ SIGNATURES = {
     "lc_gemm_set_tile": [c_int],
     "lc_gemm_set_debug": [P],
     "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float],
+    "lc_gemm_tn_ws": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float,
+                      P, c_long],
     "lc_layernorm_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_int, c_long, P, P],
     "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
     "lc_patchify": [P, c_int, c_int, c_int, P, P],

@@ -144,8 +144,10 @@ def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
                          "multiples of C's shape)")
     if colsum is not None and (colsum.dtype != F32 or colsum.numel() != N1):
         raise ValueError("colsum must be f32 [N1]")
-    call("lc_gemm_tn", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
-         float(alpha), ptr(C), C.stride(0), ptr(colsum), float(colsum_scale))
+    # the launch stream's split-K workspace takes the two-stage partials (after its tickets)
+    ws = splitk_workspace(torch.cuda.current_stream(A.device))
+    call("lc_gemm_tn_ws", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
+         float(alpha), ptr(C), C.stride(0), ptr(colsum), float(colsum_scale), ptr(ws), ws.numel())
     return C
 
 
