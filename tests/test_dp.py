@@ -1,4 +1,5 @@
-"""Data-parallel exchange (lcclip/dp.py) on CPU with the gloo backend, world_size 2.
+"""Data-parallel exchange (lcclip/dp.py) on CPU with the gloo backend, world sizes 2 and 4 (and 8
+for the prompt sharding alone, the bench's N = 8 layout: C = 10 prompts over 8 ranks).
 
 The protocol — images sharded by rank, text prompts sharded with an all-gather of the features and
 a SUM all-reduce of dL/dT, per-layer-group gradient buckets averaged at the end — is run with the
@@ -22,9 +23,8 @@ for p in (ROOT, os.path.join(ROOT, "lifelong-clip_amd")):
 
 from oracle import clip_oracle as o  # noqa: E402
 
-WORLD = 2
 B_GLOBAL = 4
-C = 3  # not a multiple of WORLD: exercises the prompt padding
+C = 3  # not a multiple of the world size: exercises the prompt padding
 
 
 def _free_port():
@@ -58,7 +58,7 @@ def _reference_grads(method):
     return grads
 
 
-def _worker(rank, port, tmpdir, method, bucket_layers):
+def _worker(rank, port, tmpdir, method, bucket_layers, WORLD):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
@@ -107,14 +107,15 @@ def _worker(rank, port, tmpdir, method, bucket_layers):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("method", ["lora", "adapter"])
-def test_dp_protocol_matches_global_batch(method):
+@pytest.mark.parametrize("method,WORLD", [("lora", 2), ("adapter", 2), ("adapter", 4)])
+def test_dp_protocol_matches_global_batch(method, WORLD):
     ref = _reference_grads(method)
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_worker, args=(_free_port(), tmp, method, 1), nprocs=WORLD, join=True)
+        mp.spawn(_worker, args=(_free_port(), tmp, method, 1, WORLD), nprocs=WORLD, join=True)
         outs = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
     # every rank ends with the same averaged gradients
-    assert torch.equal(outs[0]["flat"], outs[1]["flat"])
+    for r in range(1, WORLD):
+        assert torch.equal(outs[0]["flat"], outs[r]["flat"])
     flat = outs[0]["flat"]
     off = 0
     worst = 0.0
@@ -132,14 +133,14 @@ def test_dp_protocol_matches_global_batch(method):
     assert set(outs[0]["names"]) == set(ref.keys())
 
 
-def _slice_worker(rank, port, tmpdir):
+def _slice_worker(rank, port, tmpdir, WORLD):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     from lcclip.dp import DataParallel
     dp = DataParallel()
     res = {}
-    for Cn in (1, 2, 5, 8):
+    for Cn in (1, 2, 5, 8, 10):
         tok = torch.arange(Cn * 4).reshape(Cn, 4)
         s = dp.shard_tokens(tok)
         lo, hi, per = dp.prompt_slice(Cn)
@@ -150,11 +151,12 @@ def _slice_worker(rank, port, tmpdir):
     dist.destroy_process_group()
 
 
-def test_prompt_sharding_covers_every_prompt_once():
+@pytest.mark.parametrize("WORLD", [2, 8])
+def test_prompt_sharding_covers_every_prompt_once(WORLD):
     with tempfile.TemporaryDirectory() as tmp:
-        mp.spawn(_slice_worker, args=(_free_port(), tmp), nprocs=WORLD, join=True)
+        mp.spawn(_slice_worker, args=(_free_port(), tmp, WORLD), nprocs=WORLD, join=True)
         outs = [torch.load(os.path.join(tmp, f"s{r}.pt"), weights_only=True) for r in range(WORLD)]
-    for Cn in (1, 2, 5, 8):
+    for Cn in (1, 2, 5, 8, 10):
         tok = torch.arange(Cn * 4).reshape(Cn, 4)
         per = -(-Cn // WORLD)
         for r in range(WORLD):
