@@ -39,6 +39,10 @@ extern "C" {
 #define LC_EPI_GELU_D 6   /* out0 bf16 = QuickGELU'(pre); out1 bf16 = QuickGELU(pre), pre =    */
                           /* acc + bias: saves the derivative for the backward, not pre        */
 #define LC_EPI_MUL 7      /* out0 bf16 = alpha*acc * aux_bf16   (dX of c_fc with saved GELU')  */
+/* fp8-output epilogues (lc_gemm_nt_fp8 only): out1 = e4m3 codes + E8M0 scales (q_scale, q_rows)
+ * of the bf16-rounded result, bit-identical to the bf16 epilogue followed by lc_quant_fp8 */
+#define LC_EPI_GELU_D_Q8 12 /* out0 bf16 = QuickGELU'(pre); out1 fp8 = QuickGELU(pre)          */
+#define LC_EPI_MUL_Q8 13    /* out1 fp8 = alpha*acc * aux_bf16 (out0 unused)                   */
 
 /* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0.
  * Replaces: F.linear for QKV / out-proj (models/clip/lora.py:837, 1072; torch MHA for
@@ -67,14 +71,17 @@ int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* 
  * with A [M,K] / B [N,K] e4m3 (row strides lda / ldb in BYTES, multiples of 16) and their scales
  * sa [K/128][sa_rows][4] / sb [K/128][sb_rows][4] (sa_rows = M rounded up to 256, sb_rows >= N;
  * lc_quant_fp8 produces both). K % 128 == 0, N % 256 == 0. Epilogues LC_EPI_BF16 / F32 / RESID /
- * GELU / GELU_D / MUL as lc_gemm_nt; ws as lc_gemm_nt_ws.
+ * GELU / GELU_D / MUL as lc_gemm_nt; ws as lc_gemm_nt_ws. LC_EPI_GELU_D_Q8 / MUL_Q8 write out1 as
+ * the NEXT fp8 GEMM's A operand: codes [M, ldo1 bytes] (ldo1 % 16 == 0, 16-B aligned) and scales
+ * q_scale [N/128][q_rows][4] (q_rows = M rounded up to 256); q_scale is ignored otherwise.
  * Replaces: the fp16 frozen-backbone GEMMs of MaPLe (models/maple_clip/model.py:749-772, 826:
  * convert_weights to half; the QKV / c_fc / c_proj products of :316-401), run in fp8 as BASELINE
  * config 5 names. */
 int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                    const void* sa, long sa_rows, const void* B, long ldb, const void* sb,
                    long sb_rows, const float* bias, float alpha, void* out0, long ldo0,
-                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes);
+                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes,
+                   void* q_scale, long q_rows);
 
 /* Quantise src [rows, K] (bf16, or f32 when src_f32; element (r, k) at src[r*sr + k*sk], so a
  * transposed view quantises along its other axis) to e4m3 dst [rows, ldd] + E8M0 scales

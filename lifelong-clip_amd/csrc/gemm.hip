@@ -36,6 +36,11 @@ enum {
   EPI_AD_UP = 9,       // out0 f32 = aux_f32 + aux2_bf16 + scale * (acc + bias)
   EPI_AD_MASK = 10,    // out0 bf16 = aux_bf16 > 0 ? alpha * acc / keep : 0
   EPI_AD_ADD = 11,     // out0 bf16 = aux_bf16 + acc
+  // fp8-output epilogues of the fp8 GEMM (MaPLe's fp8 mode): out1 = e4m3 codes (ldo1 in bytes)
+  // + E8M0 scales (ep.q_scale, ep.q_rows) of the bf16-rounded value, bit-identical to the bf16
+  // epilogue followed by quant_fp8 (quant.hip) — the next fp8 GEMM's A operand straight from here
+  EPI_GELU_D_Q8 = 12,  // out0 bf16 = quick_gelu'(pre) ; out1 fp8 = quick_gelu(pre), pre = acc+bias
+  EPI_MUL_Q8 = 13,     // out1 fp8 = (acc*alpha) * aux_bf16 (out0 unused)
 };
 
 namespace {
@@ -126,7 +131,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
 #pragma unroll
   for (int q = 0; q < CPL; ++q) bb[q] = 0.f;
   if (EPI != EPI_GELU_BWD && EPI != EPI_MUL && EPI != EPI_AD_MASK && EPI != EPI_AD_ADD &&
-      bias != nullptr) {
+      EPI != EPI_MUL_Q8 && bias != nullptr) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const float4 b4 = *reinterpret_cast<const float4*>(bias + n + 4 * q);
@@ -138,7 +143,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   // issued after them would wait for their acknowledgement.
   constexpr bool AUXF = (EPI == EPI_RESID || EPI == EPI_AD_UP);
   constexpr bool AUXB = (EPI == EPI_GELU_BWD || EPI == EPI_MUL || EPI == EPI_AD_MASK ||
-                         EPI == EPI_AD_ADD);
+                         EPI == EPI_AD_ADD || EPI == EPI_MUL_Q8);
   constexpr bool AUX2 = (EPI == EPI_AD_UP);
   constexpr int NIT = PASS / RPI;
   float pf_f[2][NIT][CPL];
@@ -183,6 +188,29 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
       *reinterpret_cast<float4*>(p + 4 * q) = make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  };
+  // one lane's 8 outputs of row m as e4m3 in the fp8 operand format: the 4 lanes of a 32-column
+  // block (consecutive, 4-aligned: LPR is a multiple of 4) share one E8M0 scale; the arithmetic
+  // is quant_fp8_kernel's on the bf16-rounded values. All 4 lanes of a block hold the same row,
+  // so they skip (m >= M) together and the shuffles stay inside active lanes.
+  auto store_q8 = [&](void* base, long ld, long m, const float (&w)[CPL]) {
+    if constexpr (CPL == 8) {  // every fp8-output epilogue (no f32 output)
+      float q[8];
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        q[i] = bf2f(f2bf(w[i]));
+        amax = fmaxf(amax, fabsf(q[i]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 1));
+      amax = fmaxf(amax, __shfl_xor(amax, 2));
+      const uint32_t byte = e8m0_of(amax);
+      const float inv = e8m0_inv(byte);
+      *reinterpret_cast<uint2*>((uint8_t*)base + m * ld + n) =
+          uint2{pack4_fp8(q[0] * inv, q[1] * inv, q[2] * inv, q[3] * inv),
+                pack4_fp8(q[4] * inv, q[5] * inv, q[6] * inv, q[7] * inv)};
+      if ((lane & 3) == 0) ep.q_scale[fp8_scale_index(m, n >> 5, ep.q_rows)] = (uint8_t)byte;
+    }
   };
   // bf16 element i of a lane's packed side input
   auto bfv = [](const uint32_t* x, int i) { return bf2f((i & 1) ? (x[i >> 1] >> 16) : (x[i >> 1] & 0xffff)); };
@@ -233,7 +261,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = v[i] * quick_gelu_grad(bfv(xb, i));
         store_bf(out0, ldo0, m, w);
-      } else if constexpr (EPI == EPI_GELU_D) {
+      } else if constexpr (EPI == EPI_GELU_D || EPI == EPI_GELU_D_Q8) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) {
           const float sg = lc_sigmoid1702(v[i]);
@@ -241,11 +269,17 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
           v[i] = sg * __builtin_fmaf(1.702f * v[i], 1.0f - sg, 1.0f);  // QuickGELU'
         }
         store_bf(out0, ldo0, m, v);
-        store_bf(out1, ldo1, m, w);
-      } else if constexpr (EPI == EPI_MUL) {
+        if constexpr (EPI == EPI_GELU_D_Q8)
+          store_q8(out1, ldo1, m, w);
+        else
+          store_bf(out1, ldo1, m, w);
+      } else if constexpr (EPI == EPI_MUL || EPI == EPI_MUL_Q8) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = v[i] * bfv(xb, i);
-        store_bf(out0, ldo0, m, w);
+        if constexpr (EPI == EPI_MUL_Q8)
+          store_q8(out1, ldo1, m, w);
+        else
+          store_bf(out0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_DOWN) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = fmaxf(v[i], 0.f) * drop_mul(seed, m, n + i, ep.keep);
@@ -1710,6 +1744,8 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
     LC_G8_CASE(EPI_GELU)
     LC_G8_CASE(EPI_GELU_D)
     LC_G8_CASE(EPI_MUL)
+    LC_G8_CASE(EPI_GELU_D_Q8)
+    LC_G8_CASE(EPI_MUL_Q8)
     default:
       return LC_EINVAL;
   }
@@ -1842,19 +1878,28 @@ int lc_gemm_set_debug(unsigned long long* p) {
 int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                    const void* sa, long sa_rows, const void* B, long ldb, const void* sb,
                    long sb_rows, const float* bias, float alpha, void* out0, long ldo0,
-                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes) {
+                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes,
+                   void* q_scale, long q_rows) {
   LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 256 == 0);
   LC_CHECK_ARG(lda % 16 == 0 && ldb % 16 == 0 && lda >= K && ldb >= K);
   LC_CHECK_ARG(sa != nullptr && sb != nullptr && sa_rows >= (M + 255) / 256 * 256 &&
                sb_rows >= N && sa_rows % 256 == 0 && sb_rows % 256 == 0);
   LC_CHECK_ARG(((uintptr_t)sa & 15) == 0 && ((uintptr_t)sb & 15) == 0);
   LC_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_RESID || epi == EPI_GELU ||
-               epi == EPI_GELU_D || epi == EPI_MUL);
-  LC_CHECK_ARG(ldo0 % 8 == 0 && ldo0 >= N);
+               epi == EPI_GELU_D || epi == EPI_MUL || epi == EPI_GELU_D_Q8 || epi == EPI_MUL_Q8);
+  const bool q8 = epi == EPI_GELU_D_Q8 || epi == EPI_MUL_Q8;
+  if (epi != EPI_MUL_Q8) LC_CHECK_ARG(out0 != nullptr && ldo0 % 8 == 0 && ldo0 >= N);
   if (epi == EPI_GELU || epi == EPI_GELU_D) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
-  if (epi == EPI_RESID || epi == EPI_MUL) LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
+  // fp8 output: 8-B code stores per lane, an operand-format scale buffer covering every row
+  if (q8)
+    LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 16 == 0 && ((uintptr_t)out1 & 15) == 0 &&
+                 q_scale != nullptr && q_rows >= (M + 255) / 256 * 256 && q_rows % 256 == 0);
+  if (epi == EPI_RESID || epi == EPI_MUL || epi == EPI_MUL_Q8)
+    LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
   LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
   EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
+  ep.q_scale = q8 ? static_cast<uint8_t*>(q_scale) : nullptr;
+  ep.q_rows = q_rows;
   Fp8Scales sc{static_cast<const uint8_t*>(sa), static_cast<const uint8_t*>(sb), sa_rows, sb_rows};
   return launch_g8<true>(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                          aux, ldaux, ep, ws, ws_bytes, sc);

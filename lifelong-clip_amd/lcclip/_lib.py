@@ -23,7 +23,7 @@ SIGNATURES = {
     "lc_gemm_nt_ws": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_float, P, c_long,
                       P, c_long, P, c_long, P, c_long],
     "lc_gemm_nt_fp8": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
-                       P, c_float, P, c_long, P, c_long, P, c_long, P, c_long],
+                       P, c_float, P, c_long, P, c_long, P, c_long, P, c_long, P, c_long],
     "lc_quant_fp8": [P, c_long, c_int, P, c_int, c_long, c_long, P, c_long, P, c_long],
     "lc_gemm_set_tile": [c_int],
     "lc_gemm_set_debug": [P],

@@ -29,11 +29,13 @@ call; out-projection, attention, LayerNorm and the residual stream stay as in bf
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
 from . import ops
 from .ops import BF16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_D, EPI_MUL, EPI_RESID
+from .ops import EPI_GELU_D_Q8, EPI_MUL_Q8
 
 _seed_counter = itertools.count(1)
 
@@ -177,6 +179,14 @@ class BlockStack:
             st.q = {name: ops.quant_fp8(t, transpose=tr) for name, (t, tr) in src.items()}
             st.q_key = key
 
+    # fp8 mode: the c_fc forward and c_proj input-gradient epilogues write their result straight
+    # in the fp8 operand format of the GEMM that consumes it (EPI_GELU_D_Q8 / EPI_MUL_Q8) instead
+    # of bf16 + a quant_fp8 pass (the same codes; LCCLIP_FP8_FUSE=0 for A/Bs)
+    FUSE_Q8 = os.environ.get("LCCLIP_FP8_FUSE", "1") != "0"
+
+    def _fused_q8(self):
+        return self.precision == "fp8" and self.FUSE_Q8
+
     def _gemm(self, st, name, A, epi, out0, **kw):
         """A [M, K] bf16 @ (staged weight `name`)^T: the bf16 GEMM, or in fp8 mode for the QKV /
         c_fc / c_proj weights the fp8 GEMM on A quantised here."""
@@ -219,7 +229,8 @@ class BlockStack:
         P_of = {int(i): int(t.shape[1]) for i, t in (prompts or {}).items()}
         Mmax = n_seq * (L + max(P_of.values(), default=0))
         tmp_h = _empty((Mmax, D), BF16, dev)
-        tmp_g = _empty((Mmax, 4 * D), BF16, dev)
+        q_g = ops.Fp8Mat(Mmax, 4 * D, dev) if self._fused_q8() else None
+        tmp_g = _empty((Mmax, 4 * D), BF16, dev) if q_g is None else None
         tmp_pre = None if save else _empty((Mmax, 4 * D), BF16, dev)
         saved = [] if save else None
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
@@ -268,21 +279,27 @@ class BlockStack:
             ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
             pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
-            self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
-                       bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
+            if q_g is not None:
+                # QuickGELU(pre) only as c_proj's fp8 operand (inference discards QuickGELU')
+                g_in = ops.gemm_nt_fp8(ops.quant_fp8(th), st.q["wfc"], EPI_GELU_D_Q8, pre,
+                                       bias=blk.mlp.c_fc.bias, q_out=q_g.narrow(Mx))
+                wpr = lambda epi, out0, **kw: ops.gemm_nt_fp8(g_in, st.q["wpr"], epi, out0, **kw)  # noqa: E731
+            else:
+                self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
+                           bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
+                wpr = lambda epi, out0, **kw: self._gemm(st, "wpr", tmp_g[:Mx], epi, out0, **kw)  # noqa: E731
             x_out = _empty((Mx, D), F32, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 seed2 = next(_seed_counter) * 0x9E3779B1
                 z2 = _empty((Mx, D), BF16, dev)
-                self._gemm(st, "wpr", tmp_g[:Mx], EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
+                wpr(EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
                 hd2 = _empty((Mx, ad.down_size), BF16, dev)
                 ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
                                 s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
-                self._gemm(st, "wpr", tmp_g[:Mx], EPI_RESID, x_out, bias=blk.mlp.c_proj.bias,
-                           aux=x_mid)
+                wpr(EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
                          mean2=mean2, rstd2=rstd2, gd=pre, P=P)
@@ -324,7 +341,8 @@ class BlockStack:
         H = self.n_head
         dev = dx.device
         Mmax = n_seq * (L + max((s.get("P", 0) for s in saved), default=0))
-        da = _empty((Mmax, 4 * D), BF16, dev)
+        q_da = ops.Fp8Mat(Mmax, 4 * D, dev) if self._fused_q8() else None
+        da = _empty((Mmax, 4 * D), BF16, dev) if q_da is None else None
         dh = _empty((Mmax, D), BF16, dev)
         dO = _empty((Mmax, D), BF16, dev)
         dqkv = _empty((Mmax, 3 * D), BF16, dev)
@@ -360,8 +378,13 @@ class BlockStack:
                 dY = self._adapter_bwd(blk, st, gxb, s["hd2"], s["z2"], s["keep"], dz[:Mx], grads)
             else:
                 dY = gxb
-            self._gemm(st, "wprT", dY, EPI_MUL, da[:Mx], aux=s["gd"])
-            self._gemm(st, "wfcT", da[:Mx], EPI_BF16, dh[:Mx])
+            if q_da is not None:
+                q = ops.gemm_nt_fp8(ops.quant_fp8(dY), st.q["wprT"], EPI_MUL_Q8, None, aux=s["gd"],
+                                    q_out=q_da.narrow(Mx))
+                ops.gemm_nt_fp8(q, st.q["wfcT"], EPI_BF16, dh[:Mx])
+            else:
+                self._gemm(st, "wprT", dY, EPI_MUL, da[:Mx], aux=s["gd"])
+                self._gemm(st, "wfcT", da[:Mx], EPI_BF16, dh[:Mx])
             ops.layernorm_bwd(dh[:Mx], s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight,
                               dx_mid[:Mx], dx_midb[:Mx], dres=gx)
             # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))

@@ -10,6 +10,7 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32, EPI_GELU_D, EPI_MUL = range(8)
+EPI_GELU_D_Q8, EPI_MUL_Q8 = 12, 13  # gemm_nt_fp8 only: the result as the next fp8 GEMM's operand
 
 
 def _rowmajor(t, dtype, name):
@@ -110,23 +111,31 @@ def quant_fp8(src, out=None, transpose=False):
     return out
 
 
-def gemm_nt_fp8(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
+def gemm_nt_fp8(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None, q_out=None):
     """out = epilogue(alpha * A @ B^T + bias) with A, B Fp8Mat (block-scaled e4m3) on the fp8
-    MFMA; epilogues as gemm_nt (BF16, F32, RESID, GELU, GELU_D, MUL)."""
+    MFMA; epilogues as gemm_nt (BF16, F32, RESID, GELU, GELU_D, MUL), plus GELU_D_Q8 / MUL_Q8
+    whose fp8 result (QuickGELU(pre) / alpha*acc*aux) goes to q_out, an Fp8Mat [M, N] — the same
+    codes and scales as the bf16 epilogue followed by quant_fp8 (out0 is None for MUL_Q8)."""
     M, K = A.rows, A.K
     N = B.rows
-    if B.K != K or out0.shape[0] != M or out0.shape[1] != N:
-        raise ValueError(f"gemm_nt_fp8 shapes A[{M},{K}] B[{N},{B.K}] out{tuple(out0.shape)}")
+    q8 = epi in (EPI_GELU_D_Q8, EPI_MUL_Q8)
+    if B.K != K or (epi != EPI_MUL_Q8 and (out0.shape[0] != M or out0.shape[1] != N)):
+        raise ValueError(f"gemm_nt_fp8 shapes A[{M},{K}] B[{N},{B.K}] out"
+                         f"{None if out0 is None else tuple(out0.shape)}")
+    if q8 and (q_out is None or q_out.rows != M or q_out.K != N):
+        raise ValueError(f"gemm_nt_fp8: epilogue {epi} needs q_out Fp8Mat [{M}, {N}]")
     if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
         raise ValueError("gemm_nt_fp8 bias must be a contiguous f32 vector of length N")
+    if q8:
+        out1 = q_out.data
     st = stream_of(A.data)
     ws = splitk_workspace(torch.cuda.current_stream(A.data.device))
     call("lc_gemm_nt_fp8", st, epi, M, N, K, ptr(A.data), A.data.stride(0), ptr(A.scales),
          A.rows_pad, ptr(B.data), B.data.stride(0), ptr(B.scales), B.rows_pad, ptr(bias),
-         float(alpha), ptr(out0), out0.stride(0), ptr(out1),
+         float(alpha), ptr(out0), out0.stride(0) if out0 is not None else 0, ptr(out1),
          out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
-         ptr(ws), ws.numel())
-    return out0
+         ptr(ws), ws.numel(), ptr(q_out.scales) if q8 else None, q_out.rows_pad if q8 else 0)
+    return q_out if q8 else out0
 
 
 def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):

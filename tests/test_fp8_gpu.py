@@ -122,3 +122,37 @@ def test_gemm_fp8_epilogues(ops, dev):
     om = torch.empty(M, N, device=dev, dtype=BF)
     ops.gemm_nt_fp8(Aq, Bq, ops.EPI_MUL, om, alpha=0.5, aux=aux)
     assert rel(om, 0.5 * ref * aux.float()) < 4e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4096 + 131, 3072, 768), (1000, 768, 3072), (12608, 3072, 768)])
+def test_gemm_fp8_q8_epilogues_match_quant(ops, dev, M, N, K):
+    """The fp8-output epilogues (GELU_D_Q8 / MUL_Q8: MaPLe's c_fc forward and c_proj dX) give
+    the codes and scale bytes of the bf16 epilogue followed by quant_fp8, bit for bit, and the
+    same bf16 QuickGELU' — on ragged M, a split-K launch (K = 3072 at few tiles) and the
+    config-5 row count."""
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    A = torch.randn(M, K, device=dev, generator=g)
+    B = torch.randn(N, K, device=dev, generator=g) * K ** -0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    Aq, Bq = ops.quant_fp8(A), ops.quant_fp8(B)
+    blocks = N // 32
+
+    def same(q, ref):
+        assert torch.equal(q.data[:M].view(torch.uint8), ref.data[:M].view(torch.uint8))
+        assert torch.equal(gpu_scales(q)[:, :blocks].view(torch.uint8),
+                           gpu_scales(ref)[:, :blocks].view(torch.uint8))
+
+    gd, gl = (torch.empty(M, N, device=dev, dtype=BF) for _ in range(2))
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_GELU_D, gd, bias=bias, out1=gl)
+    gd2 = torch.empty(M, N, device=dev, dtype=BF)
+    q = ops.gemm_nt_fp8(Aq, Bq, ops.EPI_GELU_D_Q8, gd2, bias=bias,
+                        q_out=ops.Fp8Mat(M, N, dev))
+    assert torch.equal(gd2, gd)
+    same(q, ops.quant_fp8(gl))
+    aux = (torch.randn(M, N, device=dev, generator=g) * 3).to(BF)
+    aux[:, :64] = 0  # all-zero blocks: scale byte 0, codes 0
+    om = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt_fp8(Aq, Bq, ops.EPI_MUL, om, alpha=0.5, aux=aux)
+    q = ops.gemm_nt_fp8(Aq, Bq, ops.EPI_MUL_Q8, None, alpha=0.5, aux=aux,
+                        q_out=ops.Fp8Mat(M, N, dev))
+    same(q, ops.quant_fp8(om))
