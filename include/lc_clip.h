@@ -129,6 +129,17 @@ int lc_layernorm_fwd(hipStream_t stream, int rows, int D, const float* x, long l
                      const int* row_idx, const float* gamma, const float* beta, void* y,
                      int y_f32, long ldy, float* mean, float* rstd);
 
+/* The same writing the normalised rows as the A operand of an fp8 GEMM (lc_gemm_nt_fp8): e4m3
+ * codes q [rows, ldq bytes] (ldq % 16 == 0, 16-B aligned) + E8M0 scales q_scale
+ * [D/128][q_rows][4] (q_rows = rows rounded up to 256), bit-identical to the bf16 output followed
+ * by lc_quant_fp8; y (bf16, optional: NULL skips it) as lc_layernorm_fwd. D % 256 == 0.
+ * Replaces: the ln_1 / ln_2 -> fp16 GEMM input cast of MaPLe's frozen tower (BASELINE config 5
+ * fp8; models/maple_clip/model.py:316-401). */
+int lc_layernorm_fwd_fp8(hipStream_t stream, int rows, int D, const float* x, long ldx,
+                         const int* row_idx, const float* gamma, const float* beta, void* y,
+                         long ldy, float* mean, float* rstd, void* q, long ldq, void* q_scale,
+                         long q_rows);
+
 /* dx[row_idx[r]] = dres[row_idx[r]] + LayerNorm_backward(dy[r]) (gamma/beta frozen), written
  * as f32 (dx) and optionally bf16 (dx_bf16). dy is bf16 or f32 (dy_f32). dres may be NULL.
  * Replaces: autograd of F.layer_norm (model.py:199). */

@@ -66,11 +66,40 @@ LC_DEV void store_row_bf16(bf16_t* __restrict__ p, int lane, const float (&v)[V]
   }
 }
 
+// A row (V % 4 == 0 layout) as e4m3 codes + E8M0 scales in the fp8 GEMM operand format: a
+// 32-column block is 8 consecutive lanes' 4 values; the arithmetic is quant_fp8_kernel's
+// (quant.hip) on the bf16-rounded values, so the codes equal bf16 output + quant_fp8.
+template <int V>
+LC_DEV void store_row_fp8(uint8_t* __restrict__ p, uint8_t* __restrict__ scales, long rows_pad,
+                          long row, int lane, const float (&v)[V]) {
+  static_assert(V % 4 == 0, "fp8 rows need D % 256 == 0");
+#pragma unroll
+  for (int i = 0; i < V / 4; ++i) {
+    float q[4];
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q[j] = bf2f(f2bf(v[4 * i + j]));
+      amax = fmaxf(amax, fabsf(q[j]));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    amax = fmaxf(amax, __shfl_xor(amax, 4));
+    const uint32_t byte = e8m0_of(amax);
+    const float inv = e8m0_inv(byte);
+    const int k = i * 256 + lane * 4;
+    *reinterpret_cast<uint32_t*>(p + k) = pack4_fp8(q[0] * inv, q[1] * inv, q[2] * inv, q[3] * inv);
+    if ((lane & 7) == 0) scales[fp8_scale_index(row, k >> 5, rows_pad)] = (uint8_t)byte;
+  }
+}
+
+// y (bf16 / f32, optional when q is set) and / or q: the fp8 operand of the next GEMM
 template <int V>
 __global__ void __launch_bounds__(256)
 ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __restrict__ row_idx,
               const float* __restrict__ gamma, const float* __restrict__ beta, void* __restrict__ y,
-              int y_f32, long ldy, float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+              int y_f32, long ldy, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+              uint8_t* __restrict__ qo, long ldq, uint8_t* __restrict__ q_scale, long q_rows) {
   constexpr int D = V * 64;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -94,8 +123,12 @@ ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __rest
   load_row_f32<V>(beta, lane, bt);
 #pragma unroll
   for (int i = 0; i < V; ++i) v[i] = v[i] * rstd * gm[i] + bt[i];
-  if (y_f32) store_row_f32<V>((float*)y + (long)row * ldy, lane, v);
-  else store_row_bf16<V>((bf16_t*)y + (long)row * ldy, lane, v);
+  if (y != nullptr) {
+    if (y_f32) store_row_f32<V>((float*)y + (long)row * ldy, lane, v);
+    else store_row_bf16<V>((bf16_t*)y + (long)row * ldy, lane, v);
+  }
+  if constexpr (V % 4 == 0)
+    if (qo) store_row_fp8<V>(qo + (long)row * ldq, q_scale, q_rows, row, lane, v);
   if (lane == 0 && mean_out) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
@@ -227,9 +260,9 @@ int grid_for(long work, int block) {
 
 extern "C" {
 
-int lc_layernorm_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, const int* row_idx,
-                     const float* gamma, const float* beta, void* y, int y_f32, long ldy,
-                     float* mean, float* rstd) {
+static int ln_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, const int* row_idx,
+                  const float* gamma, const float* beta, void* y, int y_f32, long ldy, float* mean,
+                  float* rstd, void* q, long ldq, void* q_scale, long q_rows) {
   LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
   if (rows == 0) return LC_OK;
   dim3 grid((rows + 3) / 4), block(256);
@@ -237,7 +270,7 @@ int lc_layernorm_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, 
 #define LC_LN_F(V)                                                                               \
   case V:                                                                                       \
     hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, block, 0, st, rows, x, ldx, row_idx, gamma, beta, \
-                       y, y_f32, ldy, mean, rstd);                                              \
+                       y, y_f32, ldy, mean, rstd, (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);   \
     break;
     LC_LN_F(1) LC_LN_F(2) LC_LN_F(4) LC_LN_F(8) LC_LN_F(12) LC_LN_F(16)
     default:
@@ -245,6 +278,24 @@ int lc_layernorm_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, 
 #undef LC_LN_F
   }
   LC_LAUNCH_RET();
+}
+
+int lc_layernorm_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, const int* row_idx,
+                     const float* gamma, const float* beta, void* y, int y_f32, long ldy,
+                     float* mean, float* rstd) {
+  LC_CHECK_ARG(y != nullptr);
+  return ln_fwd(st, rows, D, x, ldx, row_idx, gamma, beta, y, y_f32, ldy, mean, rstd, nullptr, 0,
+                nullptr, 0);
+}
+
+int lc_layernorm_fwd_fp8(hipStream_t st, int rows, int D, const float* x, long ldx,
+                         const int* row_idx, const float* gamma, const float* beta, void* y,
+                         long ldy, float* mean, float* rstd, void* q, long ldq, void* q_scale,
+                         long q_rows) {
+  LC_CHECK_ARG(D % 256 == 0 && q != nullptr && q_scale != nullptr && ldq >= D && ldq % 16 == 0 &&
+               ((uintptr_t)q & 15) == 0 && q_rows >= (rows + 255) / 256 * 256 && q_rows % 256 == 0);
+  return ln_fwd(st, rows, D, x, ldx, row_idx, gamma, beta, y, 0, ldy, mean, rstd, q, ldq, q_scale,
+                q_rows);
 }
 
 int lc_layernorm_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,

@@ -31,6 +31,8 @@ SIGNATURES = {
     "lc_gemm_tn_ws": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float,
                       P, c_long],
     "lc_layernorm_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_int, c_long, P, P],
+    "lc_layernorm_fwd_fp8": [P, c_int, c_int, P, c_long, P, P, P, P, c_long, P, P, P, c_long, P,
+                             c_long],
     "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
     "lc_patchify": [P, c_int, c_int, c_int, P, P],
     "lc_vit_assemble": [P, c_int, c_int, c_int, P, P, P, P],

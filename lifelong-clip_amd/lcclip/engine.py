@@ -179,13 +179,14 @@ class BlockStack:
             st.q = {name: ops.quant_fp8(t, transpose=tr) for name, (t, tr) in src.items()}
             st.q_key = key
 
-    # fp8 mode: the c_fc forward and c_proj input-gradient epilogues write their result straight
-    # in the fp8 operand format of the GEMM that consumes it (EPI_GELU_D_Q8 / EPI_MUL_Q8) instead
-    # of bf16 + a quant_fp8 pass (the same codes; LCCLIP_FP8_FUSE=0 for A/Bs)
-    FUSE_Q8 = os.environ.get("LCCLIP_FP8_FUSE", "1") != "0"
+    # fp8 mode: the c_fc forward and c_proj input-gradient epilogues (EPI_GELU_D_Q8 /
+    # EPI_MUL_Q8) and the ln_1 / ln_2 forwards write their result straight in the fp8 operand
+    # format of the GEMM that consumes it instead of bf16 + a quant_fp8 pass (the same codes).
+    # LCCLIP_FP8_FUSE for A/Bs: 0 none, 1 the GEMM epilogues only, 2 (default) all
+    FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "2"))
 
-    def _fused_q8(self):
-        return self.precision == "fp8" and self.FUSE_Q8
+    def _fused_q8(self, level=1):
+        return self.precision == "fp8" and self.FUSE_Q8 >= level
 
     def _gemm(self, st, name, A, epi, out0, **kw):
         """A [M, K] bf16 @ (staged weight `name`)^T: the bf16 GEMM, or in fp8 mode for the QKV /
@@ -230,6 +231,7 @@ class BlockStack:
         Mmax = n_seq * (L + max(P_of.values(), default=0))
         tmp_h = _empty((Mmax, D), BF16, dev)
         q_g = ops.Fp8Mat(Mmax, 4 * D, dev) if self._fused_q8() else None
+        q_h = ops.Fp8Mat(Mmax, D, dev) if self._fused_q8(2) else None  # ln_1 / ln_2 out, fp8
         tmp_g = _empty((Mmax, 4 * D), BF16, dev) if q_g is None else None
         tmp_pre = None if save else _empty((Mmax, 4 * D), BF16, dev)
         saved = [] if save else None
@@ -255,9 +257,14 @@ class BlockStack:
             mean1 = _empty((Mx,), F32, dev)
             rstd1 = _empty((Mx,), F32, dev)
             h1 = _empty((Mx, D), BF16, dev) if (save and self.variant == "lora") else th
-            ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
             qkv = _empty((Mx, 3 * D), BF16, dev)
-            self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
+            if q_h is not None:  # bf16 h1 only when LoRA's gradient reads it
+                qa = ops.layernorm_fwd_fp8(x, blk.ln_1.weight, blk.ln_1.bias, q_h.narrow(Mx),
+                                           mean1, rstd1, y=None if h1 is th else h1)
+                ops.gemm_nt_fp8(qa, st.q["wqkv"], EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
+            else:
+                ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
+                self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
             O = _empty((Mx, D), BF16, dev)
             lse = _empty((n_seq * H, Lx), F32, dev)
             ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
@@ -276,15 +283,22 @@ class BlockStack:
                 ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
             mean2 = _empty((Mx,), F32, dev)
             rstd2 = _empty((Mx,), F32, dev)
-            ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
             pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
             if q_g is not None:
-                # QuickGELU(pre) only as c_proj's fp8 operand (inference discards QuickGELU')
-                g_in = ops.gemm_nt_fp8(ops.quant_fp8(th), st.q["wfc"], EPI_GELU_D_Q8, pre,
+                # ln_2 and QuickGELU(pre) only as the fp8 operands of c_fc / c_proj (inference
+                # discards QuickGELU')
+                if q_h is not None:
+                    qa = ops.layernorm_fwd_fp8(x_mid, blk.ln_2.weight, blk.ln_2.bias,
+                                               q_h.narrow(Mx), mean2, rstd2)
+                else:
+                    ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
+                    qa = ops.quant_fp8(th)
+                g_in = ops.gemm_nt_fp8(qa, st.q["wfc"], EPI_GELU_D_Q8, pre,
                                        bias=blk.mlp.c_fc.bias, q_out=q_g.narrow(Mx))
                 wpr = lambda epi, out0, **kw: ops.gemm_nt_fp8(g_in, st.q["wpr"], epi, out0, **kw)  # noqa: E731
             else:
+                ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
                 self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
                            bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
                 wpr = lambda epi, out0, **kw: self._gemm(st, "wpr", tmp_g[:Mx], epi, out0, **kw)  # noqa: E731

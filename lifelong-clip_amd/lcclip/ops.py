@@ -170,6 +170,19 @@ def layernorm_fwd(x, weight, bias, y, mean=None, rstd=None, row_idx=None):
     return y
 
 
+def layernorm_fwd_fp8(x, weight, bias, q, mean=None, rstd=None, y=None):
+    """LayerNorm of x [rows, D] f32 straight into q, an Fp8Mat [rows, D] (the next fp8 GEMM's
+    A operand; the codes of bf16 output + quant_fp8); y: optional bf16 copy."""
+    _rowmajor(x, F32, "x")
+    rows, D = x.shape
+    if q.rows != rows or q.K != D or (y is not None and (y.dtype != BF16 or y.shape != x.shape)):
+        raise ValueError("layernorm_fwd_fp8: output shape mismatch")
+    call("lc_layernorm_fwd_fp8", stream_of(x), rows, D, ptr(x), x.stride(0), None, ptr(weight),
+         ptr(bias), ptr(y), y.stride(0) if y is not None else 0, ptr(mean), ptr(rstd), ptr(q.data),
+         q.data.stride(0), ptr(q.scales), q.rows_pad)
+    return q
+
+
 def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_idx=None):
     rows = dy.shape[0]
     D = x.shape[1]

@@ -156,3 +156,25 @@ def test_gemm_fp8_q8_epilogues_match_quant(ops, dev, M, N, K):
     q = ops.gemm_nt_fp8(Aq, Bq, ops.EPI_MUL_Q8, None, alpha=0.5, aux=aux,
                         q_out=ops.Fp8Mat(M, N, dev))
     same(q, ops.quant_fp8(om))
+
+
+@pytest.mark.parametrize("rows,D", [(12608, 768), (300, 1024), (77, 256)])
+def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D):
+    """LayerNorm straight into the fp8 operand format (MaPLe's ln_1 / ln_2 in fp8 mode) equals
+    the bf16 LayerNorm followed by quant_fp8 bit for bit, with the same saved statistics."""
+    g = torch.Generator(device=dev).manual_seed(rows + D)
+    x = torch.randn(rows, D, device=dev, generator=g) * 3 + 1
+    x[5] = 0  # a constant row: all-zero normalised blocks when beta is 0 there
+    w = torch.randn(D, device=dev, generator=g)
+    b = torch.randn(D, device=dev, generator=g)
+    b[:32] = 0
+    y = torch.empty(rows, D, device=dev, dtype=BF)
+    m1, r1 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    ops.layernorm_fwd(x, w, b, y, m1, r1)
+    ref = ops.quant_fp8(y)
+    m2, r2 = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    y2 = torch.empty_like(y)
+    q = ops.layernorm_fwd_fp8(x, w, b, ops.Fp8Mat(rows, D, dev), m2, r2, y=y2)
+    assert torch.equal(q.data, ref.data)
+    assert torch.equal(gpu_scales(q), gpu_scales(ref))
+    assert torch.equal(y2, y) and torch.equal(m2, m1) and torch.equal(r2, r1)
