@@ -173,6 +173,15 @@ int lc_attn_fwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, lo
 int lc_attn_bwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
                 const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
                 int causal);
+/* The backward with dq|dk|dv written as the A operand of the fp8 QKV input-gradient GEMM
+ * (lc_gemm_nt_fp8): e4m3 codes dqkv [n_seq*L, lddq BYTES] (lddq % 16 == 0, 16-B aligned) + E8M0
+ * scales q_scale [3*H*64/128][q_rows][4] (q_rows = n_seq*L rounded up to 256), bit-identical to
+ * lc_attn_bwd followed by lc_quant_fp8. L <= 224 (the fused single-pass kernel).
+ * Replaces: the same backward feeding MaPLe's fp16 in-proj input gradient
+ * (models/maple_clip/model.py:316-401, BASELINE config 5 in fp8). */
+int lc_attn_bwd_fp8(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
+                    const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
+                    void* q_scale, long q_rows, int causal);
 
 /* GPU train transform of the online step: the torchvision Compose of methods/_trainer.py:212-242
  * as applied to the batch at methods/adapter_clip.py:81 — optional uint8 round trip of the

@@ -405,12 +405,16 @@ struct BwdLds {
 // item's Q / dO / O / lse rows and K / V fragments are loaded into registers while the current
 // one computes (rows after the current item's LDS image is written, K / V after its phase 1), so
 // the item's HBM traffic (~230 KB at L = 197) overlaps the MFMA / exp work of the previous one.
-template <int NQB, bool PERSIST = (NQB >= 5)>
+//
+// Q8: dQ / dK / dV written as the A operand of the fp8 QKV input-gradient GEMM (MaPLe's fp8
+// mode): e4m3 codes (lddq in bytes) + E8M0 scales (q_scale, q_rows), the arithmetic of
+// quant_fp8_kernel on the bf16-rounded values, so the codes equal bf16 output + quant_fp8.
+template <int NQB, bool PERSIST = (NQB >= 5), bool Q8 = false>
 __global__ void __launch_bounds__(64 * NQB)
 attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
                    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
                    const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, int causal,
-                   float scale) {
+                   float scale, uint8_t* __restrict__ q_scale = nullptr, long q_rows = 0) {
   constexpr int LP = 32 * NQB;
   constexpr int NTH = 64 * NQB;
   using Lay = BwdLds<NQB>;
@@ -483,6 +487,39 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   load_o(item);
   load_kv(item);
 
+  // one row's 64 head columns (lane g holds columns dt*16 + 4g + {0..3} in x[dt], the 4 lanes
+  // t, t+16, t+32, t+48 share the row) times mul, to dqkv columns col0..col0+63
+  auto put_row = [&](long row, int col0, f32x4 x0, f32x4 x1, f32x4 x2, f32x4 x3, float mul) {
+    const f32x4 x[4] = {x0, x1, x2, x3};
+    if constexpr (!Q8) {
+      bf16_t* dst = dqkv + row * lddq + col0;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<uint2*>(dst + dt * 16 + 4 * g) =
+            uint2{pack2bf(x[dt][0] * mul, x[dt][1] * mul), pack2bf(x[dt][2] * mul, x[dt][3] * mul)};
+    } else {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(dqkv) + row * lddq + col0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {  // 32-column scale blocks: dt = 2b, 2b + 1
+        float v[8];
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          v[i] = bf2f(f2bf(x[2 * b + (i >> 2)][i & 3] * mul));
+          amax = fmaxf(amax, fabsf(v[i]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 16));
+        amax = fmaxf(amax, __shfl_xor(amax, 32));
+        const uint32_t byte = e8m0_of(amax);
+        const float inv = e8m0_inv(byte);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<uint32_t*>(dst + (2 * b + j) * 16 + 4 * g) =
+              pack4_fp8(v[4 * j] * inv, v[4 * j + 1] * inv, v[4 * j + 2] * inv, v[4 * j + 3] * inv);
+        if (g == 0) q_scale[fp8_scale_index(row, (col0 >> 5) + b, q_rows)] = (uint8_t)byte;
+      }
+    }
+  };
 #pragma unroll 1
   for (; item < n_items; item += gridDim.x) {
   const int next = item + gridDim.x;
@@ -584,16 +621,9 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
 #pragma unroll
   for (int k2 = 0; k2 < 2; ++k2) {
     const int key = kb + k2 * 16 + t;
-    if (key < L) {
-      bf16_t* dst = dqkv + (base + key) * lddq + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 a = dK[dt][k2], b = dV[dt][k2];
-        *reinterpret_cast<uint2*>(dst + D + dt * 16 + 4 * g) =
-            uint2{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale)};
-        *reinterpret_cast<uint2*>(dst + 2 * D + dt * 16 + 4 * g) =
-            uint2{pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
-      }
+    if (key < L) {  // every lane of the row (same t) takes this branch together
+      put_row(base + key, D + h * 64, dK[0][k2], dK[1][k2], dK[2][k2], dK[3][k2], scale);
+      put_row(base + key, 2 * D + h * 64, dV[0][k2], dV[1][k2], dV[2][k2], dV[3][k2], 1.0f);
     }
   }
   __syncthreads();  // every wave is done with Qs -> reuse it for K
@@ -643,15 +673,7 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = qb + qt * 16 + t;
-    if (q < L) {
-      bf16_t* dst = dqkv + (base + q) * lddq + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const f32x4 a = dQ[dt][qt];
-        *reinterpret_cast<uint2*>(dst + dt * 16 + 4 * g) =
-            uint2{pack2bf(a[0] * scale, a[1] * scale), pack2bf(a[2] * scale, a[3] * scale)};
-      }
-    }
+    if (q < L) put_row(base + q, h * 64, dQ[0][qt], dQ[1][qt], dQ[2][qt], dQ[3][qt], scale);
   }
   if constexpr (!PERSIST) break;  // one item per workgroup (short sequences: many workgroups)
   __syncthreads();  // phase 2 done with Ks / dS^T before the next item's LDS image
@@ -826,6 +848,32 @@ int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
     break;
     LC_AF(1) LC_AF(2) LC_AF(3) LC_AF(4) LC_AF(5) LC_AF(6) LC_AF(7) LC_AF(8)
 #undef LC_AF
+    default:
+      return LC_EINVAL;
+  }
+  LC_LAUNCH_RET();
+}
+
+int lc_attn_bwd_fp8(hipStream_t st, int n_seq, int L, int H, const void* qkv, long ldq,
+                    const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
+                    void* q_scale, long q_rows, int causal) {
+  LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 224 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
+  LC_CHECK_ARG(lddq >= 3 * H * 64 && lddq % 16 == 0 && ((uintptr_t)dqkv & 15) == 0 &&
+               ldq % 8 == 0 && ldo % 8 == 0 && q_scale != nullptr && q_rows % 256 == 0 &&
+               q_rows >= ((long)n_seq * L + 255) / 256 * 256);
+  const int D = H * 64;
+  const float scale = 0.125f;
+  switch ((L + 31) / 32) {
+#define LC_ABQ(Q)                                                                               \
+  case Q:                                                                                      \
+    hipLaunchKernelGGL((attn_bwd_kernel<Q, (Q >= 5), true>),                                   \
+                       dim3(Q >= 5 ? persistent_grid(n_seq * H, BwdLds<Q>::BYTES) : n_seq * H),  \
+                       dim3(64 * Q), 0, st, n_seq * H, L, H, D, (const bf16_t*)qkv, ldq,        \
+                       (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, (bf16_t*)dqkv, lddq,      \
+                       causal, scale, (uint8_t*)q_scale, q_rows);                               \
+    break;
+    LC_ABQ(1) LC_ABQ(2) LC_ABQ(3) LC_ABQ(4) LC_ABQ(5) LC_ABQ(6) LC_ABQ(7)
+#undef LC_ABQ
     default:
       return LC_EINVAL;
   }

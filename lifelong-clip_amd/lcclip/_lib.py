@@ -40,6 +40,8 @@ SIGNATURES = {
     "lc_eot_rows": [P, c_int, c_int, P, P],
     "lc_attn_fwd": [P, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int],
     "lc_attn_bwd": [P, c_int, c_int, c_int, P, c_long, P, P, c_long, P, P, c_long, c_int],
+    "lc_attn_bwd_fp8": [P, c_int, c_int, c_int, P, c_long, P, P, c_long, P, P, c_long, P, c_long,
+                        c_int],
     "lc_train_transform": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, P,
                            P, c_int, c_int, c_int, P],
     "lc_autoaugment": [P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
@@ -83,7 +85,10 @@ def load(path: str = None):
         raise LcError(f"liblcclip.so not built at {path}; run `python __graft_entry__.py build` "
                       "(there is no CPU fallback)")
     lib = ctypes.CDLL(path)
+    ab = path != LIB_PATH  # an older A/B build may lack newer entry points: those stay unbound
     for name, argtypes in SIGNATURES.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)  # AttributeError if the symbol is missing
         fn.argtypes = argtypes
         fn.restype = c_int

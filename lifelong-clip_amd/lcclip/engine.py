@@ -180,10 +180,11 @@ class BlockStack:
             st.q_key = key
 
     # fp8 mode: the c_fc forward and c_proj input-gradient epilogues (EPI_GELU_D_Q8 /
-    # EPI_MUL_Q8) and the ln_1 / ln_2 forwards write their result straight in the fp8 operand
-    # format of the GEMM that consumes it instead of bf16 + a quant_fp8 pass (the same codes).
-    # LCCLIP_FP8_FUSE for A/Bs: 0 none, 1 the GEMM epilogues only, 2 (default) all
-    FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "2"))
+    # EPI_MUL_Q8), the ln_1 / ln_2 forwards and the attention backward write their result
+    # straight in the fp8 operand format of the GEMM that consumes it instead of bf16 + a
+    # quant_fp8 pass (the same codes). LCCLIP_FP8_FUSE for A/Bs: 0 none, 1 the GEMM epilogues,
+    # 2 + LayerNorm, 3 (default) + attention backward
+    FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "3"))
 
     def _fused_q8(self, level=1):
         return self.precision == "fp8" and self.FUSE_Q8 >= level
@@ -356,6 +357,9 @@ class BlockStack:
         dev = dx.device
         Mmax = n_seq * (L + max((s.get("P", 0) for s in saved), default=0))
         q_da = ops.Fp8Mat(Mmax, 4 * D, dev) if self._fused_q8() else None
+        # the attention backward's dq|dk|dv as the fp8 QKV dX operand (LoRA reads them in bf16)
+        fuse_attn = self._fused_q8(3) and self.variant != "lora" and Mmax // n_seq <= 224
+        q_dqkv = ops.Fp8Mat(Mmax, 3 * D, dev) if fuse_attn else None
         da = _empty((Mmax, 4 * D), BF16, dev) if q_da is None else None
         dh = _empty((Mmax, D), BF16, dev)
         dO = _empty((Mmax, D), BF16, dev)
@@ -416,14 +420,23 @@ class BlockStack:
             if self.variant == "lora":
                 self._lora_grad(dY, s["O"], attn.out_proj.lora_A, attn.out_proj.lora_B,
                                 attn.scaling, grads, st.lora_out)
-            ops.attn_bwd(s["qkv"], s["O"], dO[:Mx], s["lse"], dqkv[:Mx], n_seq, Lx, H, self.causal)
+            if q_dqkv is not None and not first:
+                qd = ops.attn_bwd_fp8(s["qkv"], s["O"], dO[:Mx], s["lse"], q_dqkv.narrow(Mx), n_seq,
+                                      Lx, H, self.causal)
+            else:
+                qd = None
+                ops.attn_bwd(s["qkv"], s["O"], dO[:Mx], s["lse"], dqkv[:Mx], n_seq, Lx, H,
+                             self.causal)
             if self.variant == "lora":
                 self._lora_grad(dqkv[:Mx], s["h1"], attn.in_proj_weight_lora_A,
                                 attn.in_proj_weight_lora_B, attn.scaling, grads, st.lora_in)
             if first:
                 self._layer_done(li, grad_stream, on_layer)
                 break
-            self._gemm(st, "wqkvT", dqkv[:Mx], EPI_BF16, dh[:Mx])
+            if qd is not None:
+                ops.gemm_nt_fp8(qd, st.q["wqkvT"], EPI_BF16, dh[:Mx])
+            else:
+                self._gemm(st, "wqkvT", dqkv[:Mx], EPI_BF16, dh[:Mx])
             ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
                               oxb, dres=dx_mid[:Mx])
             ev = self._layer_done(li, grad_stream, on_layer)

@@ -236,6 +236,19 @@ def attn_bwd(qkv, O, dO, lse, dqkv, n_seq, L, H, causal):
     return dqkv
 
 
+def attn_bwd_fp8(qkv, O, dO, lse, q, n_seq, L, H, causal):
+    """attn_bwd with dq|dk|dv written straight into q, an Fp8Mat [n_seq*L, 3*H*64] (the fp8
+    QKV input-gradient GEMM's A operand; the codes of attn_bwd + quant_fp8). L <= 224."""
+    if O.stride(0) != dO.stride(0):
+        raise ValueError("O and dO must share a row stride")
+    if q.rows != n_seq * L or q.K != 3 * H * 64:
+        raise ValueError("attn_bwd_fp8: output shape mismatch")
+    call("lc_attn_bwd_fp8", stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), ptr(dO),
+         O.stride(0), ptr(lse), ptr(q.data), q.data.stride(0), ptr(q.scales), q.rows_pad,
+         int(causal))
+    return q
+
+
 def cast_bf16(src, dst):
     if src.dtype != F32 or not src.is_contiguous() or not dst.is_contiguous():
         raise ValueError("cast_bf16 expects contiguous f32 -> bf16")

@@ -178,3 +178,25 @@ def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D):
     assert torch.equal(q.data, ref.data)
     assert torch.equal(gpu_scales(q), gpu_scales(ref))
     assert torch.equal(y2, y) and torch.equal(m2, m1) and torch.equal(r2, r1)
+
+
+@pytest.mark.parametrize("n_seq,L,H,causal", [(4, 197, 12, False), (2, 199, 12, False),
+                                              (3, 77, 8, True), (2, 40, 2, False)])
+def test_attn_bwd_fp8_matches_quant(ops, dev, n_seq, L, H, causal):
+    """The attention backward writing dq|dk|dv as the fp8 QKV-dX operand (MaPLe's fp8 mode)
+    equals attn_bwd followed by quant_fp8 bit for bit: persistent (L = 197, 199) and
+    one-item-per-workgroup (L = 77 causal, 40) variants."""
+    g = torch.Generator(device=dev).manual_seed(n_seq * L + H)
+    D = H * 64
+    M = n_seq * L
+    qkv = torch.randn(M, 3 * D, device=dev, generator=g).to(BF)
+    O = torch.empty(M, D, device=dev, dtype=BF)
+    lse = torch.empty(n_seq * H, L, device=dev)
+    ops.attn_fwd(qkv, O, lse, n_seq, L, H, causal)
+    dO = torch.randn(M, D, device=dev, generator=g).to(BF)
+    dqkv = torch.empty(M, 3 * D, device=dev, dtype=BF)
+    ops.attn_bwd(qkv, O, dO, lse, dqkv, n_seq, L, H, causal)
+    ref = ops.quant_fp8(dqkv)
+    q = ops.attn_bwd_fp8(qkv, O, dO, lse, ops.Fp8Mat(M, 3 * D, dev), n_seq, L, H, causal)
+    assert torch.equal(q.data, ref.data)
+    assert torch.equal(gpu_scales(q), gpu_scales(ref))
