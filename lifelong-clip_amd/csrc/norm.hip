@@ -105,8 +105,11 @@ ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __rest
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const long src = row_idx ? (long)row_idx[row] : (long)row;
-  float v[V];
+  // every load of the row issued before the first reduction: one HBM round trip per row
+  float v[V], gm[V], bt[V];
   load_row_f32<V>(x + src * ldx, lane, v);
+  load_row_f32<V>(gamma, lane, gm);
+  load_row_f32<V>(beta, lane, bt);
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < V; ++i) s += v[i];
@@ -118,9 +121,6 @@ ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __rest
     q += v[i] * v[i];
   }
   const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
-  float gm[V], bt[V];
-  load_row_f32<V>(gamma, lane, gm);
-  load_row_f32<V>(beta, lane, bt);
 #pragma unroll
   for (int i = 0; i < V; ++i) v[i] = v[i] * rstd * gm[i] + bt[i];
   if (y != nullptr) {
@@ -153,6 +153,9 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   else load_row_bf16<V>((const bf16_t*)dy + (long)row * ldy, lane, g);
   load_row_f32<V>(x + xr * ldx, lane, xv);
   load_row_f32<V>(gamma, lane, gm);
+  // the residual gradient too, before the reductions (it was a second exposed round trip)
+  float r[V];
+  if (dres) load_row_f32<V>(dres + xr * ldo, lane, r);
   const float mu = mean[row], rs = rstd[row];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -168,8 +171,6 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
 #pragma unroll
   for (int i = 0; i < V; ++i) out[i] = rs * (g[i] - s1 - xv[i] * s2);
   if (dres) {
-    float r[V];
-    load_row_f32<V>(dres + xr * ldo, lane, r);
 #pragma unroll
     for (int i = 0; i < V; ++i) out[i] += r[i];
   }
