@@ -10,6 +10,7 @@
 //  AdamW (torch.optim.AdamW as selected by utils/train_utils.py:27-28) over one flat fp32
 //        buffer holding every trainable tensor, with the GradScaler-style non-finite skip.
 #include "lc_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -227,37 +228,242 @@ lora_grad_kernel(int M, int N, int K, const bf16_t* __restrict__ dY, long ldy,
 }
 
 // ---------------------------------------------------------------------------- adapter
-// 64 rows per workgroup, 4 waves x 16 rows, everything in registers:
-//   down  D^T[j][m] = sum_k Wd[j][k] z[m][k]      (A = Wd rows, B = z rows; K = width)
-//   h = dropout(relu(D + bd))                      (lane holds 4 consecutive j of one row m)
-//   up    U^T[n][m] = sum_j Wu[n][j] h[m][j]       (B = h straight from the accumulators; the
-//                                                    A fragment reads Wu in the same j order)
-//   x_out = resid + z + scale*(U + bu)             (adapter.py:59-72, model.py:440-441)
 constexpr int AD_H = 64;  // adapter.py:38 hard-codes the down width (Q7)
 
-// k-order used when an accumulator pair (tiles 2s, 2s+1) becomes a B operand:
-// slot j<4 -> 32s + 4g + j ; j>=4 -> 32s + 16 + 4g + (j-4)
-LC_DEV bf16x8 load_perm(const bf16_t* row, int s, int g) {
-  const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * g);
-  const uint2 hi = *reinterpret_cast<const uint2*>(row + 32 * s + 16 + 4 * g);
-  bf16x8 r;
-  r[0] = (short)(lo.x & 0xffff); r[1] = (short)(lo.x >> 16);
-  r[2] = (short)(lo.y & 0xffff); r[3] = (short)(lo.y >> 16);
-  r[4] = (short)(hi.x & 0xffff); r[5] = (short)(hi.x >> 16);
-  r[6] = (short)(hi.y & 0xffff); r[7] = (short)(hi.y >> 16);
-  return r;
+// ------------------------------------------------------------ adapter backward, one pass
+// dpre = (h > 0) ? scale * (g Wu) / keep : 0   [M, 64]   (adapter.py:59-72 autograd: the ReLU
+// dz   = g + dpre Wd                           [M, D]    mask, dropout and up-projection scale)
+// Row-block walker: a persistent workgroup (8 waves, two per SIMD) per CU streams 32-row blocks
+// of g through a 3-deep LDS ring (two blocks in flight behind the one computing); both weights
+// stay in registers for the whole launch (MFMA fragments staged once through LDS), and g is read
+// from HBM once for both products (the two-GEMM form reads it twice and round-trips dpre).
+// Arithmetic is the GEMM epilogues' (EPI_AD_MASK, EPI_AD_ADD) with the same MFMA operand order
+// and k order, so the results are bit-identical to that path.
+//   phase 1: dpre^T[j][m]: wave w owns the 16x16 tile j = 16 (w & 3) .., m = 16 (w >> 2) ..
+//   phase 2: dz^T[n][m] (K = 64): wave w owns n-tiles w ND/2 .. +ND/2-1 for both row tiles;
+//            dz is written over g in the LDS image and stored as whole rows
+// The g image is row-major with 16-B units XOR-swizzled by (row & 15), so the 16 rows an MFMA
+// fragment read touches land in distinct banks.
+constexpr int AD_MT = 2;          // 16-row tiles per block
+constexpr int AD_R = 16 * AD_MT;  // rows per block
+constexpr int AD_NS = 3;          // ring depth
+constexpr int AD_NW = 8;          // waves
+template <int ND>
+struct AdBwdLds {
+  static constexpr int D = 64 * ND;
+  static constexpr int XB = AD_R * D * 2;               // one g block (bf16)
+  static constexpr int HB = AD_R * AD_H * 2;            // one h block
+  static constexpr int X0 = 0, H0 = AD_NS * XB, S0 = H0 + AD_NS * HB;
+  static constexpr int BYTES = S0 + AD_R * AD_H * 2;    // + the dpre block (phase-2 operand)
+  static_assert(AD_NS * XB >= AD_H * D * 2, "the weight staging reuses the g ring");
+};
+
+LC_DEV int ad_swz(int row, int unit) { return unit ^ (row & 15); }
+LC_DEV int ad_swz_s(int row, int unit) { return unit ^ ((row >> 1) & 7); }
+template <int N>
+LC_DEV void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-LC_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
-  uint32_t w0 = pack2bf(a[0], a[1]), w1 = pack2bf(a[2], a[3]);
-  uint32_t w2 = pack2bf(b[0], b[1]), w3 = pack2bf(b[2], b[3]);
-  bf16x8 r;
-  r[0] = (short)(w0 & 0xffff); r[1] = (short)(w0 >> 16);
-  r[2] = (short)(w1 & 0xffff); r[3] = (short)(w1 >> 16);
-  r[4] = (short)(w2 & 0xffff); r[5] = (short)(w2 >> 16);
-  r[6] = (short)(w3 & 0xffff); r[7] = (short)(w3 >> 16);
-  return r;
+// s_waitcnt vmcnt(n) for a count known only at run time (the ring's ramp-up / drain)
+LC_DEV void wait_vm_dyn(int n) {
+  switch (n) {
+#define LC_WV(k) case k: wait_vm<k>(); break;
+    LC_WV(0) LC_WV(1) LC_WV(2) LC_WV(3) LC_WV(4) LC_WV(5) LC_WV(6) LC_WV(7) LC_WV(8) LC_WV(9)
+    LC_WV(10) LC_WV(11) LC_WV(12) LC_WV(13) LC_WV(14) LC_WV(15) LC_WV(16) LC_WV(17) LC_WV(18)
+    LC_WV(19) LC_WV(20) LC_WV(21) LC_WV(22) LC_WV(23) LC_WV(24) LC_WV(25) LC_WV(26) LC_WV(27)
+    LC_WV(28) LC_WV(29) LC_WV(30) LC_WV(31)
+#undef LC_WV
+    default: wait_vm<0>(); break;
+  }
 }
 
+template <int ND, bool DZ>
+__global__ void __launch_bounds__(64 * AD_NW, 1)
+adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
+                         const bf16_t* __restrict__ Hs, const bf16_t* __restrict__ WuT,
+                         const bf16_t* __restrict__ WdT, float scale, float keep,
+                         bf16_t* __restrict__ dpre, bf16_t* __restrict__ dz, long ldz) {
+  using Lay = AdBwdLds<ND>;
+  constexpr int D = Lay::D, RU = D / 8;  // 16-B units per g row
+  constexpr int NT2 = ND / 2;            // phase-2 n-tiles per wave
+  __shared__ __attribute__((aligned(16))) char smem[Lay::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int t = lane & 15, g = lane >> 4;
+  const int nt1 = w & 3, mt1 = w >> 2;
+  const int nb = (M + AD_R - 1) / AD_R;
+  int blk = blockIdx.x;
+  if (blk >= nb) return;
+
+  // g block: wave w fills 1-KiB pieces w*XP .. +XP-1; LDS unit u = piece*64 + lane holds row
+  // u / RU, source unit (u % RU) ^ (row & 15). h block: 2 x 256 B per wave (4-B lanes), linear.
+  constexpr int XP = Lay::XB / 1024 / AD_NW, HP = Lay::HB / 256 / AD_NW;
+  static_assert(XP * 1024 * AD_NW == Lay::XB && HP * 256 * AD_NW == Lay::HB, "even split");
+  auto dma_block = [&](int b, int slot) {
+    char* xs = smem + Lay::X0 + slot * Lay::XB;
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int piece = w * XP + i, u = piece * 64 + lane;
+      const int row = u / RU, cu = ad_swz(row, u % RU);
+      const int r = min(b * AD_R + row, M - 1);  // tail rows: computed, never stored
+      glds16(G + (long)r * ldg + cu * 8, xs + piece * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < HP; ++i) {
+      const int piece = w * HP + i, e = piece * 64 + lane;  // 4-B element pairs
+      const int row = e >> 5;
+      const int r = min(b * AD_R + row, M - 1);
+      glds4(Hs + (long)r * AD_H + (e & 31) * 2, smem + Lay::H0 + slot * Lay::HB + piece * 256);
+    }
+  };
+
+  // prologue: both weights' fragments into registers, staged through the (still free) ring
+  bf16x8 wu[2 * ND];  // Wu^T rows 16 nt1 + t, k-slice ks
+  bf16x8 wd[NT2][2];  // Wd^T rows (w NT2 + j) 16 + t, k-slice ks
+  {
+    constexpr int UP = AD_H * D * 2 / 1024 / AD_NW;  // Wu^T [64][D], linear
+#pragma unroll
+    for (int i = 0; i < UP; ++i) {
+      const int piece = w * UP + i;
+      glds16(WuT + (long)(piece * 64 + lane) * 8, smem + piece * 1024);
+    }
+    wait_vm<0>();
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2 * ND; ++ks)
+      wu[ks] = *reinterpret_cast<const bf16x8*>(smem + (16 * nt1 + t) * (D * 2) + (ks * 4 + g) * 16);
+    __syncthreads();
+  }
+  if constexpr (DZ) {
+    constexpr int WP = D * AD_H * 2 / 1024 / AD_NW;  // Wd^T [D][64], linear
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int piece = w * WP + i;
+      glds16(WdT + (long)(piece * 64 + lane) * 8, smem + piece * 1024);
+    }
+    wait_vm<0>();
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NT2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int n = (w * NT2 + j) * 16 + t;
+        wd[j][ks] = *reinterpret_cast<const bf16x8*>(smem + n * 128 + (ks * 4 + g) * 16);
+      }
+    __syncthreads();  // every wave holds its fragments before the ring is overwritten
+  }
+  // ring: this walker's blocks i = 0 .. n-1 (block blockIdx.x + i * gridDim.x) in slot i % NS;
+  // the prologue issues blocks 0 .. NS-2, iteration i issues block i + NS - 1 after its barrier
+  // and then stores block i. Issue order per wave: D0 .. D(P-1), then per iteration D(i+P), S(i)
+  // (P = NS - 1), so when iteration i waits for Di the memory ops issued after it are
+  // min(P-1, n-1-i) later blocks' DMAs (LP each) and min(i, P) blocks' stores (SP each).
+  constexpr int P = AD_NS - 1, LP = XP + HP, SP = 1 + (DZ ? XP : 0);
+  static_assert((P - 1) * LP + P * SP < 32, "wait_vm_dyn range");
+  const int n = (nb - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+    if (i < n) dma_block(blk + i * gridDim.x, i);
+  const float inv = 1.0f / keep;
+#pragma unroll 1
+  for (int i = 0; i < n; ++i, blk += gridDim.x) {
+    const int slot = i % AD_NS;
+    // block i's DMA landed; the barrier also retires every wave's use of the slot the next DMA
+    // overwrites (block i-1's) and of the dpre image
+    wait_vm_dyn(min(P - 1, n - 1 - i) * LP + min(i, P) * SP);
+    __syncthreads();
+    if (i + P < n) dma_block(blk + P * gridDim.x, (i + P) % AD_NS);
+    char* xs = smem + Lay::X0 + slot * Lay::XB;
+    const char* hs = smem + Lay::H0 + slot * Lay::HB;
+    {
+      // phase 1: lane holds dpre^T[j = 16 nt1 + 4g + r][m = 16 mt1 + t]
+      const int row = 16 * mt1 + t, m = blk * AD_R + row;
+      const char* xrow = xs + row * (D * 2);
+      f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2 * ND; ++ks) {
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(xrow + ad_swz(t, ks * 4 + g) * 16);
+        a1 = mfma16(wu[ks], fb, a1);
+        // at most 6 fragment reads hoisted ahead (the weights already hold 144 registers)
+        if (ks % 6 == 5) __builtin_amdgcn_sched_barrier(0);
+      }
+      // EPI_AD_MASK: v = acc * scale (+ no bias); (h > 0) ? v / keep : 0
+      const int col = 16 * nt1 + 4 * g;
+      const uint2 hb = *reinterpret_cast<const uint2*>(hs + row * 128 + col * 2);
+      const uint32_t hh[2] = {hb.x, hb.y};
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float hv = bf2f((r & 1) ? (hh[r >> 1] >> 16) : (hh[r >> 1] & 0xffff));
+        const float v = a1[r] * scale + 0.0f;
+        o[r] = hv > 0.f ? v * inv : 0.f;
+      }
+      const uint2 ob = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+      if (m < M) *reinterpret_cast<uint2*>(dpre + (long)m * AD_H + col) = ob;
+      if constexpr (DZ)
+        *reinterpret_cast<uint2*>(smem + Lay::S0 + row * 128 + ad_swz_s(row, col >> 3) * 16 +
+                                  (col & 7) * 2) = ob;
+    }
+    if constexpr (DZ) {
+      __syncthreads();  // the whole dpre block is in LDS; phase 1's g reads are done
+#pragma unroll
+      for (int mt = 0; mt < AD_MT; ++mt) {
+        const int row = 16 * mt + t;
+        bf16x8 fs[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fs[ks] = *reinterpret_cast<const bf16x8*>(smem + Lay::S0 + row * 128 +
+                                                    ad_swz_s(row, ks * 4 + g) * 16);
+        char* xrow = xs + row * (D * 2);
+        constexpr int JH = NT2 % 2 == 0 ? NT2 / 2 : NT2;  // tiles in flight (register budget)
+#pragma unroll
+        for (int j0 = 0; j0 < NT2; j0 += JH) {
+        f32x4 a2[NT2];
+#pragma unroll
+        for (int j = j0; j < j0 + JH; ++j) {
+          a2[j] = mfma16(wd[j][0], fs[0], f32x4{0.f, 0.f, 0.f, 0.f});
+          a2[j] = mfma16(wd[j][1], fs[1], a2[j]);
+        }
+#pragma unroll
+        for (int j = j0; j < j0 + JH; ++j) {
+          // EPI_AD_ADD: g + acc; lane holds dz[m][n = 16 (w NT2 + j) + 4g + r], written over its
+          // own g values in the image (each element is read and rewritten by the same lane)
+          const int n = (w * NT2 + j) * 16 + 4 * g;
+          uint2* gp = reinterpret_cast<uint2*>(xrow + ad_swz(t, n >> 3) * 16 + (n & 7) * 2);
+          const uint2 gb = *gp;
+          const uint32_t gg[2] = {gb.x, gb.y};
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            o[r] = bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff)) + (a2[j][r] * 1.0f + 0.0f);
+          *gp = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+        }
+        }
+      }
+      __syncthreads();  // the dz block is complete in the image
+      // whole-row stores: wave w writes the image's 1-KiB pieces w*XP .. (16 B per lane)
+#pragma unroll
+      for (int i2 = 0; i2 < XP; ++i2) {
+        const int piece = w * XP + i2, u = piece * 64 + lane;
+        const int row = u / RU, cu = ad_swz(row, u % RU);
+        const int m = blk * AD_R + row;
+        const uint4 v = *reinterpret_cast<const uint4*>(xs + piece * 1024 + lane * 16);
+        if (m < M) *reinterpret_cast<uint4*>(dz + (long)m * ldz + cu * 8) = v;
+      }
+    }
+  }
+}
+
+int ad_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    n = v;
+  }
+  return n;
+}
 
 // ---------------------------------------------------------------------------- AdamW
 __global__ void finite_kernel(long n, const float* __restrict__ g, int* __restrict__ flag) {
@@ -387,6 +593,28 @@ int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, con
                    void* dz, long ldz) {
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
+  // one-pass row-block kernel at the towers' widths (LC_ADAPTER_FUSED=0: the two-GEMM form)
+  const char* fe = getenv("LC_ADAPTER_FUSED");  // read per call: tests compare both forms
+  const bool fused = fe == nullptr || atoi(fe) != 0;
+  // (dpre alone stays on the GEMM: 17.6 vs 22.8 us standalone; with dz 40.4 vs 44.9 us)
+  if (fused && dz != nullptr && (D == 768 || D == 512) && M >= 1024 && ((uintptr_t)gout & 15) == 0 &&
+      ((uintptr_t)h & 15) == 0 && ((uintptr_t)WuT & 15) == 0 && ((uintptr_t)WdT & 15) == 0) {
+    const int nb = (M + AD_R - 1) / AD_R;
+    const dim3 grid(nb < ad_cu_count() ? nb : ad_cu_count()), block(64 * AD_NW);
+    auto G = static_cast<const bf16_t*>(gout);
+    auto H = static_cast<const bf16_t*>(h);
+    auto U = static_cast<const bf16_t*>(WuT);
+    auto Wd = static_cast<const bf16_t*>(WdT);
+    auto P = static_cast<bf16_t*>(dpre);
+    auto Z = static_cast<bf16_t*>(dz);
+#define LC_ADB(ND, DZ)                                                                            \
+  hipLaunchKernelGGL((adapter_bwd_fused_kernel<ND, DZ>), grid, block, 0, st, M, G, ldg, H, U, Wd, \
+                     scale, keep, P, Z, ldz)
+    if (D == 768) LC_ADB(12, true);
+    else LC_ADB(8, true);
+#undef LC_ADB
+    LC_LAUNCH_RET();
+  }
   EpiParams ep{nullptr, 0, scale, keep, 0, nullptr};
   int rc = lc_gemm_nt_ex(st, 10 /*EPI_AD_MASK*/, M, AD_H, D, gout, ldg, WuT, D, nullptr, scale, dpre,
                          AD_H, nullptr, 0, h, AD_H, ep);

@@ -381,7 +381,8 @@ def test_transform_patches_feed_the_image_tower(dev):
 
 
 # ------------------------------------------------------------------------------- PEFT
-@pytest.mark.parametrize("D,M,keep", [(768, 1000, 1.0), (128, 77, 1.0), (512, 300, 0.9)])
+@pytest.mark.parametrize("D,M,keep", [(768, 1000, 1.0), (128, 77, 1.0), (512, 300, 0.9),
+                                      (768, 4109, 0.9), (512, 2000, 1.0)])
 def test_adapter_fwd_bwd(ops, dev, D, M, keep):
     torch.manual_seed(4)
     z = torch.randn(M, D, device=dev).to(BF)
@@ -412,6 +413,32 @@ def test_adapter_fwd_bwd(ops, dev, D, M, keep):
     dpr = torch.where(h.float() > 0, dh / keep, torch.zeros_like(dh))
     assert rel(dpre, dpr) < 4e-3
     assert rel(dz, g.float() + dpre.float() @ Wd.float()) < 4e-3
+
+
+@pytest.mark.parametrize("D,M,with_dz", [(768, 50432, True), (768, 4109, True), (768, 1031, True),
+                                         (512, 2013, True), (768, 4109, False)])
+def test_adapter_bwd_fused_matches_gemms(ops, dev, D, M, with_dz, monkeypatch):
+    """The one-pass adapter backward (row-block walker, M >= 1024 at D = 768 / 512) gives the
+    two-GEMM form's dpre and dz bit for bit (same MFMA operand and k order, same epilogue
+    arithmetic): ragged last block, a walker with a single block, the step's row count; and the
+    dpre-only call (routed to the GEMM either way)."""
+    torch.manual_seed(D + M)
+    g = torch.randn(M, D, device=dev).to(BF)
+    h = torch.relu(torch.randn(M, 64, device=dev)).to(BF)
+    Wu = (torch.randn(D, 64, device=dev) * 0.125).to(BF)
+    Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
+    WuT, WdT = Wu.t().contiguous(), Wd.t().contiguous()
+    outs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("LC_ADAPTER_FUSED", mode)
+        dpre = torch.full((M, 64), 7.0, device=dev, dtype=BF)
+        dz = torch.full((M, D), 7.0, device=dev, dtype=BF) if with_dz else None
+        ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz)
+        torch.cuda.synchronize()
+        outs[mode] = (dpre, dz)
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    if with_dz:
+        assert torch.equal(outs["1"][1], outs["0"][1])
 
 
 def test_lora_merge_and_grad(ops, dev):
