@@ -107,6 +107,9 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   constexpr int NW = WM * WN;
+#if defined(G8_NOSTORE) && G8_NOSTORE == 1  // diagnostic builds only: epilogue off (results wrong)
+  if (ep.dbg == nullptr) return;
+#endif
   // Through LDS. The swapped MFMA leaves 4 consecutive columns of one row per lane, so
   // a direct store would touch 16 rows x 64 B per instruction. Each wave instead parks 32 rows
   // of its accumulator tile in the (now idle) stage ring and reads them back row-contiguous:
@@ -241,6 +244,9 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       }
       const float* xf = pf_f[pass & 1][it];
       const uint32_t* xb = pf_b[pass & 1][it];
+#if defined(G8_NOSTORE) && G8_NOSTORE == 2  // diagnostic builds only: global stores off
+      if (ep.dbg == nullptr) continue;
+#endif
       if (m >= M) continue;
       float w[CPL];
       if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
