@@ -20,6 +20,11 @@ struct TfParams {
   float inv_std[4], nbias[4];  // 1/std and -mean/std (the LDS kernel's fused normalise)
 };
 
+// One bilinear blend a (1 - l) + b l as an explicit FMA on the rounded first product, so every
+// kernel (f32 NCHW, patch rows, separable) rounds the same way: the f32 image and the patch rows
+// stay bit-identical whichever kernel wrote them.
+LC_DEV float lerp1(float a, float b, float l) { return __builtin_fmaf(b, l, a * (1.f - l)); }
+
 // torch upsample_bilinear2d (align_corners = False) source index and weight along one axis
 LC_DEV void lin_src(int dst, float scale, int in, int& i0, int& i1, float& l1) {
   float src = scale * (dst + 0.5f) - 0.5f;
@@ -75,9 +80,7 @@ train_transform_kernel(int n, int C, int Hin, int Win, const float* __restrict__
         lin_src(px, sw, Win, x0, x1, lx);
         const float a = quant(src[y0 * Win + x0], quantize), b = quant(src[y0 * Win + x1], quantize);
         const float cc = quant(src[y1 * Win + x0], quantize), d = quant(src[y1 * Win + x1], quantize);
-        const float top = a * (1.f - lx) + b * lx;
-        const float bot = cc * (1.f - lx) + d * lx;
-        val = top * (1.f - ly) + bot * ly;
+        val = lerp1(lerp1(a, b, lx), lerp1(cc, d, lx), ly);
       }
       v[k] = (val - tp.mean[c]) / tp.std_[c];
     }
@@ -115,9 +118,9 @@ LC_DEV void tf_row(const float* __restrict__ simg, const Tap& ry, const Tap (&cx
   for (int k = 0; k < NV; ++k) {
     float val = 0.f;
     if (ry.ok & cx[k].ok) {
-      const float top = r0[cx[k].i0] * (1.f - cx[k].l1) + r0[cx[k].i1] * cx[k].l1;
-      const float bot = r1[cx[k].i0] * (1.f - cx[k].l1) + r1[cx[k].i1] * cx[k].l1;
-      val = top * (1.f - ry.l1) + bot * ry.l1;
+      const float top = lerp1(r0[cx[k].i0], r0[cx[k].i1], cx[k].l1);
+      const float bot = lerp1(r1[cx[k].i0], r1[cx[k].i1], cx[k].l1);
+      val = lerp1(top, bot, ry.l1);
     }
     v[k] = __builtin_fmaf(val, inv, bias);
   }
@@ -191,6 +194,75 @@ train_transform_lds_kernel(int C, int Hin, int Win, const float* __restrict__ x,
   }
 }
 
+// Separable form of the layout-1 (conv1 patch rows) transform, one workgroup per (image,
+// channel): the horizontal pass runs once per SOURCE row — Hs[i][x] = r_i[c0(x)] (1 - lx) +
+// r_i[c1(x)] lx for the Hin source rows and the R output columns (crop, flip and zero fill
+// folded into the column taps) — and every output pixel is then Hs[y0][x] (1 - ly) + Hs[y1][x] ly,
+// read as two 16-B LDS vectors per 8 pixels. Same f32 operations in the same order as tf_row
+// (lerp1 top / bottom per source row, then the vertical lerp1 and the normalising FMA: the f32
+// image through lc_patchify and these patch rows are bit-identical); the LDS-read
+// count per pixel drops from 4 scalar reads to 0.5 vector reads, which bounded tf_row's kernel
+// (1.7 TB/s of output). Output: 8 bf16 (16 B) per lane, lanes in patch-row order (512 B runs).
+__global__ void __launch_bounds__(256)
+train_transform_sep_kernel(int C, int Hin, int Win, const float* __restrict__ x, int R, int pad,
+                           int crop_i, int crop_j, int flip, TfParams tp, int quantize,
+                           bf16_t* __restrict__ out) {
+  extern __shared__ float sep_lds[];
+  const int img = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int npx = Hin * Win;
+  float* simg = sep_lds;                               // [Hin][Win]
+  float* hs = sep_lds + ((npx + 3) & ~3);              // [Hin][R]
+  Tap* rows = reinterpret_cast<Tap*>(hs + Hin * R);    // [R]
+  Tap* cols = rows + R;                                // [R]
+  const float* src = x + ((long)img * C + c) * npx;
+  for (int k = tid; k < npx; k += blockDim.x) simg[k] = quant(src[k], quantize);
+  const float sh = (float)Hin / (float)R, sw = (float)Win / (float)R;
+  for (int k = tid; k < 2 * R; k += blockDim.x) {
+    const bool is_row = k < R;
+    const int o = is_row ? k : k - R;
+    const int p = is_row ? o + crop_i - pad : (flip ? R - 1 - o : o) + crop_j - pad;
+    Tap t{0, 0, 0.f, 0};
+    if (p >= 0 && p < R) {
+      lin_src(p, is_row ? sh : sw, is_row ? Hin : Win, t.i0, t.i1, t.l1);
+      t.ok = 1;
+    }
+    (is_row ? rows : cols)[o] = t;
+  }
+  __syncthreads();
+  for (int k = tid; k < Hin * R; k += blockDim.x) {
+    const int i = k / R, xo = k - i * R;
+    const Tap t = cols[xo];
+    const float* r = simg + i * Win;
+    hs[k] = t.ok ? lerp1(r[t.i0], r[t.i1], t.l1) : 0.f;
+  }
+  __syncthreads();
+  constexpr int P = 16;
+  const int g = R / P;
+  const float inv = tp.inv_std[c], bias = tp.nbias[c];
+  const long row_len = (long)C * P * P;
+  bf16_t* o = out + (long)img * g * g * row_len + c * P * P;
+  // chunk = ((pyi * g + pxi) * P + ky) * 2 + half: 8 output columns of one patch row
+  for (int ch = tid; ch < g * g * P * 2; ch += blockDim.x) {
+    const int half = ch & 1, ky = (ch >> 1) & (P - 1), pq = ch >> 5;
+    const int pyi = pq / g, pxi = pq - pyi * g;
+    const int y = pyi * P + ky, x0 = pxi * P + half * 8;
+    const Tap ry = rows[y];
+    const float4* a = reinterpret_cast<const float4*>(hs + ry.i0 * R + x0);
+    const float4* b = reinterpret_cast<const float4*>(hs + ry.i1 * R + x0);
+    const float4 t0 = a[0], t1 = a[1], u0 = b[0], u1 = b[1];
+    const float top[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    const float bot[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float val = ry.ok ? lerp1(top[k], bot[k], ry.l1) : 0.f;
+      v[k] = __builtin_fmaf(val, inv, bias);
+    }
+    *reinterpret_cast<uint4*>(o + (long)pq * row_len + ky * P + half * 8) =
+        uint4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -216,6 +288,15 @@ int lc_train_transform(hipStream_t st, int n, int C, int Hin, int Win, const flo
     hipLaunchKernelGGL(train_transform_lds_kernel<0>, dim3(n, 8),  // 8 workgroups per image
                        dim3(nrg * q4), img_bytes, st, C,
                        Hin, Win, x, R, pad, crop_i, crop_j, flip, tp, quantize, out);
+    LC_LAUNCH_RET();
+  }
+  // conv1 patch rows (the product path): the separable kernel when a channel's source rows
+  // resized to R columns fit in LDS beside the channel (CIFAR: 4 + 28 + 7 KB)
+  const size_t sep_bytes =
+      (size_t)(((Hin * Win + 3) & ~3) + Hin * R) * sizeof(float) + 2 * (size_t)R * sizeof(Tap);
+  if (layout == 1 && patch == 16 && R % 16 == 0 && sep_bytes <= 64 * 1024) {
+    hipLaunchKernelGGL(train_transform_sep_kernel, dim3(n, C), dim3(256), sep_bytes, st, C, Hin,
+                       Win, x, R, pad, crop_i, crop_j, flip, tp, quantize, static_cast<bf16_t*>(out));
     LC_LAUNCH_RET();
   }
   if (img_bytes <= 64 * 1024 && layout == 1 && patch == 16 && C * 32 <= 256) {
