@@ -78,6 +78,22 @@ LC_DEV int tr_off(int t, int g, int dt) {
   return row * 128 + swz(row, col >> 3) * 16 + (col & 7) * 2;
 }
 
+// One output row's 64 head columns from the 4 lanes t + 16g that share it (lane g: packed bf16 of
+// columns dt*16 + 4g .. +3 in x[dt]) as two 16-B stores per lane instead of four 8-B ones: one
+// v_permlane16_swap per dword exchanges lane groups 1 <-> 0 and 3 <-> 2 between the column-tile
+// pairs (0, 1) and (2, 3), after which group g holds columns 32p + 16(g & 1) + 8(g >> 1) .. +7
+// of pair p (the epilogue store tail is issue-bound: half the store instructions, same bytes).
+// All four lanes of the row must be active (row guards are uniform over them).
+LC_DEV void store_row64(bf16_t* row, int g, const uint2 (&x)[4]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const auto s0 = __builtin_amdgcn_permlane16_swap(x[2 * p].x, x[2 * p + 1].x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(x[2 * p].y, x[2 * p + 1].y, false, false);
+    *reinterpret_cast<uint4*>(row + 32 * p + 16 * (g & 1) + 8 * (g >> 1)) =
+        uint4{s0[0], s1[0], s0[1], s1[1]};
+  }
+}
+
 constexpr int V_STRIDE = 160;  // bytes per V row in the forward's plain V image (conflict-free tr)
 
 // ----------------------------------------------------------------------------------- forward
@@ -221,12 +237,13 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
     const int q = qb + qt * 16 + t;
     if (q < L) {
       const float inv = 1.0f / l;
+      uint2 x[4];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const f32x4 o = Oa[dt][qt];
-        *reinterpret_cast<uint2*>(O + (base + q) * ldo + h * 64 + dt * 16 + 4 * g) =
-            uint2{pack2bf(o[0] * inv, o[1] * inv), pack2bf(o[2] * inv, o[3] * inv)};
+        x[dt] = uint2{pack2bf(o[0] * inv, o[1] * inv), pack2bf(o[2] * inv, o[3] * inv)};
       }
+      store_row64(O + (base + q) * ldo + h * 64, g, x);
       if (g == 0) lse[(long)nh * L + q] = mx[qt] + __log2f(l);
     }
   }
@@ -492,11 +509,11 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   auto put_row = [&](long row, int col0, f32x4 x0, f32x4 x1, f32x4 x2, f32x4 x3, float mul) {
     const f32x4 x[4] = {x0, x1, x2, x3};
     if constexpr (!Q8) {
-      bf16_t* dst = dqkv + row * lddq + col0;
+      uint2 xp[4];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        *reinterpret_cast<uint2*>(dst + dt * 16 + 4 * g) =
-            uint2{pack2bf(x[dt][0] * mul, x[dt][1] * mul), pack2bf(x[dt][2] * mul, x[dt][3] * mul)};
+        xp[dt] = uint2{pack2bf(x[dt][0] * mul, x[dt][1] * mul), pack2bf(x[dt][2] * mul, x[dt][3] * mul)};
+      store_row64(dqkv + row * lddq + col0, g, xp);
     } else {
       uint8_t* dst = reinterpret_cast<uint8_t*>(dqkv) + row * lddq + col0;
 #pragma unroll
@@ -835,7 +852,7 @@ extern "C" {
 int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long ldq, void* O,
                 long ldo, float* lse, int causal) {
   LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 256 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
-  LC_CHECK_ARG(ldq % 8 == 0 && ldo % 8 == 0);
+  LC_CHECK_ARG(ldq % 8 == 0 && ldo % 8 == 0 && ((uintptr_t)O & 15) == 0);  // 16-B row stores
   const int D = H * 64;
   const int nqb = (L + 31) / 32;
   dim3 grid(n_seq * H);
@@ -883,7 +900,8 @@ int lc_attn_bwd_fp8(hipStream_t st, int n_seq, int L, int H, const void* qkv, lo
 int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long ldq, const void* O,
                 const void* dO, long ldo, const float* lse, void* dqkv, long lddq, int causal) {
   LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 256 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
-  LC_CHECK_ARG(lddq >= 3 * H * 64 && ldq % 8 == 0 && ldo % 8 == 0 && lddq % 8 == 0);
+  LC_CHECK_ARG(lddq >= 3 * H * 64 && ldq % 8 == 0 && ldo % 8 == 0 && lddq % 8 == 0 &&
+               ((uintptr_t)dqkv & 15) == 0);  // 16-B row stores
   const int D = H * 64;
   const int nqb = (L + 31) / 32;
   dim3 grid(n_seq * H);
