@@ -166,7 +166,7 @@ int lc_eot_rows(hipStream_t stream, int C, int L, const int64_t* tokens, int* ro
 /* Multi-head attention core, d_head = 64, L <= 256. qkv [n_seq*L, ldq] holds
  * q|k|v at columns 0, H*64, 2*H*64; O [n_seq*L, ldo]; lse f32 [n_seq*H, L] (log2 domain).
  * ldq, ldo, lddq % 8 == 0; O and dqkv 16-B aligned (each row's 64 head columns are written as
- * 16-B pieces). */
+ * 16-B pieces).
  * causal = 1 applies the text tower's upper-triangular -inf mask.
  * Replaces: lora.py:950-1071 (q scaling, bmm, mask, softmax, dropout p=0, bmm) and the SDPA
  * path of torch nn.MultiheadAttention (model.py:217,230), forward and backward. */
