@@ -180,9 +180,8 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   // one lane's CPL outputs of row m: a single 8-B / 16-B bf16 store, or NQ 16-B f32 stores
   auto store_bf = [&](void* base, long ld, long m, const float (&w)[CPL]) {
     bf16_t* p = (bf16_t*)base + m * ld + n;
-    if constexpr (CPL == 8)
-      *reinterpret_cast<uint4*>(p) = uint4{pack2bf(w[0], w[1]), pack2bf(w[2], w[3]),
-                                           pack2bf(w[4], w[5]), pack2bf(w[6], w[7])};
+    if constexpr (CPL == 8)  // nontemporal: the consumer is the next kernel (st_nt16)
+      st_nt16(p, pack2bf(w[0], w[1]), pack2bf(w[2], w[3]), pack2bf(w[4], w[5]), pack2bf(w[6], w[7]));
     else
       *reinterpret_cast<uint2*>(p) = uint2{pack2bf(w[0], w[1]), pack2bf(w[2], w[3])};
   };
