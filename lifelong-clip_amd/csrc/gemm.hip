@@ -159,7 +159,10 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       if constexpr (AUXF) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          const float4 f = *reinterpret_cast<const float4*>((const float*)aux + m * ldaux + n + 4 * q);
+          // side inputs are read once: nontemporal (step +0.5 %, tools/gpu_ab_lib.sh V=NTL)
+          const f32x4 fv = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>((const float*)aux + m * ldaux + n + 4 * q));
+          const float4 f = make_float4(fv[0], fv[1], fv[2], fv[3]);
           pf_f[slot][it][4 * q] = f.x, pf_f[slot][it][4 * q + 1] = f.y;
           pf_f[slot][it][4 * q + 2] = f.z, pf_f[slot][it][4 * q + 3] = f.w;
         }
@@ -168,7 +171,8 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
         const bf16_t* bsrc = AUXB ? (const bf16_t*)aux + m * ldaux + n
                                   : (const bf16_t*)ep.aux2 + m * ep.ldaux2 + n;
         if constexpr (CPL == 8) {
-          const uint4 u = *reinterpret_cast<const uint4*>(bsrc);
+          const i32x4 uv = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(bsrc));
+          const uint4 u = make_uint4(uv[0], uv[1], uv[2], uv[3]);
           pf_b[slot][it][0] = u.x, pf_b[slot][it][1] = u.y, pf_b[slot][it][2] = u.z, pf_b[slot][it][3] = u.w;
         } else {
           const uint2 u = *reinterpret_cast<const uint2*>(bsrc);
