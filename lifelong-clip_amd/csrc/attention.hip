@@ -61,8 +61,12 @@ LC_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return as_bf8(u32x4{pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])});
 }
 
+// q / k / v, O and dO rows are read once per (sequence, head): nontemporal (step +0.4 %,
+// tools/gpu_ab_libs.sh VS=ATL)
 LC_DEV uint4 ld16_or_zero(const bf16_t* p, bool ok) {
-  return ok ? *reinterpret_cast<const uint4*>(p) : uint4{0, 0, 0, 0};
+  if (!ok) return uint4{0, 0, 0, 0};
+  const i32x4 v = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));
+  return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
 // Lane offsets (bytes) into a swizzled 128-B-row image, valid for any row block that starts at a

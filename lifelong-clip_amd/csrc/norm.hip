@@ -151,7 +151,16 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   float g[V], xv[V], gm[V];
   if (dy_f32) load_row_f32<V>((const float*)dy + (long)row * ldy, lane, g);
   else load_row_bf16<V>((const bf16_t*)dy + (long)row * ldy, lane, g);
-  load_row_f32<V>(x + xr * ldx, lane, xv);
+  // the forward's saved input, read once: nontemporal (step +0.5 %, tools/gpu_ab_libs.sh VS=LNL)
+  if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i) {
+      const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + xr * ldx + i * 256 + lane * 4));
+      xv[4 * i] = t[0]; xv[4 * i + 1] = t[1]; xv[4 * i + 2] = t[2]; xv[4 * i + 3] = t[3];
+    }
+  } else {
+    load_row_f32<V>(x + xr * ldx, lane, xv);
+  }
   load_row_f32<V>(gamma, lane, gm);
   // the residual gradient too, before the reductions (it was a second exposed round trip)
   float r[V];
