@@ -56,10 +56,6 @@ LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 LC_DEV void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 16, 0, 0);
 }
-// nontemporal form (cache policy NT): a streamed operand each byte of which is read once
-LC_DEV void glds16_nt(const void* gsrc, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 16, 0, 2);
-}
 // 4-byte form: LDS destination = wave-uniform base + lane * 4.
 LC_DEV void glds4(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 4, 0, 0);
