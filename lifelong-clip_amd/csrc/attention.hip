@@ -62,7 +62,7 @@ LC_DEV bf16x8 pack8(const f32x4& a, const f32x4& b) {
 }
 
 // q / k / v, O and dO rows are read once per (sequence, head): nontemporal (step +0.4 %,
-// tools/gpu_ab_libs.sh VS=ATL)
+// profiles/r02/epilogue_knockout.txt)
 LC_DEV uint4 ld16_or_zero(const bf16_t* p, bool ok) {
   if (!ok) return uint4{0, 0, 0, 0};
   const i32x4 v = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(p));

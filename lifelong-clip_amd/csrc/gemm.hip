@@ -159,7 +159,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       if constexpr (AUXF) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          // side inputs are read once: nontemporal (step +0.5 %, tools/gpu_ab_lib.sh V=NTL)
+          // side inputs are read once: nontemporal (step +0.5 %, profiles/r02/epilogue_knockout.txt)
           const f32x4 fv = __builtin_nontemporal_load(
               reinterpret_cast<const f32x4*>((const float*)aux + m * ldaux + n + 4 * q));
           const float4 f = make_float4(fv[0], fv[1], fv[2], fv[3]);

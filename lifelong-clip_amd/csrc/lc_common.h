@@ -13,7 +13,7 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));  // 32 fp8 e4m3 (one 16x16x128 operand)
 
 // 16-B nontemporal (streaming) global store: a large producer output that the next kernel reads
-// once. Measured on the step's GEMM epilogues (tools/gpu_ntst.sh): c_fc + QuickGELU/' 297 -> 269 us,
+// once. Measured on the step's GEMM epilogues: c_fc + QuickGELU/' 297 -> 269 us,
 // QKV fwd 171 -> 162 us, step +1.6 % (profiles/r02/epilogue_knockout.txt).
 __device__ __forceinline__ void st_nt16(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   __builtin_nontemporal_store(i32x4{(int)a, (int)b, (int)c, (int)d}, reinterpret_cast<i32x4*>(p));

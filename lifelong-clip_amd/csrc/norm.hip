@@ -151,7 +151,7 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   float g[V], xv[V], gm[V];
   if (dy_f32) load_row_f32<V>((const float*)dy + (long)row * ldy, lane, g);
   else load_row_bf16<V>((const bf16_t*)dy + (long)row * ldy, lane, g);
-  // the forward's saved input, read once: nontemporal (step +0.5 %, tools/gpu_ab_libs.sh VS=LNL)
+  // the forward's saved input, read once: nontemporal (step +0.5 %, profiles/r02/epilogue_knockout.txt)
   if constexpr (V % 4 == 0) {
 #pragma unroll
     for (int i = 0; i < V / 4; ++i) {
