@@ -448,23 +448,51 @@ autoaug_kernel(int C, int H, int W, const float* __restrict__ x, float* __restri
       __syncthreads();
       for (int k = tid; k < tot; k += blockDim.x) atomicAdd(&hist[(k / HW) * 256 + a[k]], 1);
       __syncthreads();
-      if (tid < C) {
-        int* h = hist + tid * 256;
-        int last = 255;
-        while (last > 0 && h[last] == 0) --last;  // the last non-zero bin
-        int sum = 0;
-        for (int k = 0; k < last; ++k) sum += h[k];
+      // one wave per channel, 4 bins per lane: the last non-zero bin (max), the sum below it and
+      // the cumulative sum (wave scans) instead of three 256-step serial loops with a division each
+      const int wv = tid >> 6, ln = tid & 63;
+      if (wv < C) {
+        int* h = hist + wv * 256;
+        int hv[4], lastl = -1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hv[j] = h[4 * ln + j];
+          if (hv[j] != 0) lastl = 4 * ln + j;
+        }
+        int last = lastl;  // the last non-zero bin (0 when none)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o));
+        last = last < 0 ? 0 : last;
+        int part = 0, cl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          part += (4 * ln + j < last) ? hv[j] : 0;
+          cl[j] = (j ? cl[j - 1] : 0) + hv[j];  // lane-local inclusive cumsum
+        }
+        int sum = part;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
         const int step = sum / 255;
         if (step == 0) {
-          for (int k = 0; k < 256; ++k) h[k] = k;  // unchanged channel
+#pragma unroll
+          for (int j = 0; j < 4; ++j) h[4 * ln + j] = 4 * ln + j;  // unchanged channel
         } else {
-          int cum = 0, prev = 0;
-          for (int k = 0; k < 256; ++k) {
-            cum += h[k];
-            const int v = (cum + step / 2) / step;  // lut before the shift
-            h[k] = prev;                            // pad [1, 0], drop the last
-            prev = v > 255 ? 255 : v;
+          int off = cl[3];  // inclusive scan of the lane totals, then exclusive
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(off, o);
+            if (ln >= o) off += y;
           }
+          off -= cl[3];
+          int lut[4];  // lut before the shift: (cumsum + step // 2) // step, clamped
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lut[j] = min((off + cl[j] + step / 2) / step, 255);
+          int prev = __shfl_up(lut[3], 1);  // pad [1, 0], drop the last
+          if (ln == 0) prev = 0;
+          h[4 * ln] = prev;
+          h[4 * ln + 1] = lut[0];
+          h[4 * ln + 2] = lut[1];
+          h[4 * ln + 3] = lut[2];
         }
       }
       __syncthreads();
