@@ -18,12 +18,10 @@ import os
 import sys
 import time
 
-# HIP hardware queues per process (HIP's default is 4). The step runs three streams of its own
-# (main chain, text tower, PEFT weight gradients) and RCCL adds its own once the process group is
-# up: at 4 queues the side streams then share the main stream's queue and stop overlapping it
-# (measured at N = 1 with the exchange forced on: 7308 img/s at 4 queues, 8172 at 8; without
-# the process group 8223 / 8256). Set before anything initialises HIP.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP hardware queues per process: left at the runtime's setting (HIP's default is 4, the GPU
+# box's too) and recorded in the output line. With the process group up the trainer shares one
+# side stream between the text tower and the PEFT weight gradients so that main + side + RCCL fit
+# in 4 queues (OnlineTrainer._merge_side_streams).
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "lifelong-clip_amd")):
@@ -82,6 +80,8 @@ class GemmTimer:
         self.records = []
 
     def __enter__(self):
+        main = torch.cuda.current_stream()
+
         def timed(A, B, epi, out0, **kw):
             st = torch.cuda.current_stream()
             e0 = torch.cuda.Event(enable_timing=True)
@@ -96,7 +96,8 @@ class GemmTimer:
                 t = kw.get(extra)
                 if t is not None:
                     nbytes += t.numel() * t.element_size()
-            self.records.append((e0, e1, 2.0 * M * N * K, nbytes, routes_to_pp(M, N, K, epi)))
+            self.records.append((e0, e1, 2.0 * M * N * K, nbytes, routes_to_pp(M, N, K, epi),
+                                 st == main))
             return r
         self.ops.gemm_nt = timed
         import lcclip.engine as eng
@@ -107,18 +108,27 @@ class GemmTimer:
         self.ops.gemm_nt = self.orig
 
     def summary(self):
+        """Sums over the step's GEMM launches. `pp_*`: the dominant-kernel launches on the main
+        (image-chain) stream only — side-stream launches (text tower, PEFT weight gradients) run
+        concurrently with them, so their durations are reported apart (`side_ms`) and never summed
+        into a share of the step."""
         torch.cuda.synchronize()
-        ms = sum(r[0].elapsed_time(r[1]) for r in self.records)
-        pp = [(r[0].elapsed_time(r[1]), r[2], r[3]) for r in self.records if r[4]]
-        return dict(n=len(self.records), ms=ms, pp_n=len(pp), pp_ms=sum(t for t, _, _ in pp),
+        main = [r for r in self.records if r[5]]
+        ms = sum(r[0].elapsed_time(r[1]) for r in main)
+        side_ms = sum(r[0].elapsed_time(r[1]) for r in self.records if not r[5])
+        pp = [(r[0].elapsed_time(r[1]), r[2], r[3]) for r in main if r[4]]
+        return dict(n=len(main), ms=ms, side_n=len(self.records) - len(main), side_ms=side_ms,
+                    pp_n=len(pp), pp_ms=sum(t for t, _, _ in pp),
                     pp_flops=sum(f for _, f, _ in pp), pp_bytes=sum(b for _, _, b in pp))
 
 
 class TowerTimer:
     """HIP events (torch's current stream, where the image tower launches) around the image
-    tower's forward and backward inside one step: the SURVEY §8(d) north-star ratio
-    B * F_img / (t_image_tower * peak), text tower and head excluded. The backward span ends
-    after the side-stream PEFT weight gradients have joined (they are image-tower work)."""
+    tower's forward and backward of every step of the timed loop: the SURVEY §8(d) north-star
+    ratio B * F_img / (t_image_tower * peak), text tower and head excluded. The backward span
+    ends after the side-stream PEFT weight gradients have joined (they are image-tower work).
+    Events are recorded inside the back-to-back loop that `value` times (no synchronize before
+    a step), so a step's tower time is its share of that loop; the median over steps is reported."""
 
     def __init__(self, tower):
         self.tower = tower
@@ -145,8 +155,15 @@ class TowerTimer:
         self.tower.forward, self.tower.backward = self.fwd, self.bwd
 
     def ms(self):
+        """Per-step tower time (fwd + bwd spans; two spans per step), median over the steps."""
         torch.cuda.synchronize()
-        return sum(e0.elapsed_time(e1) for e0, e1 in self.spans)
+        per = [self.spans[i][0].elapsed_time(self.spans[i][1]) +
+               self.spans[i + 1][0].elapsed_time(self.spans[i + 1][1])
+               for i in range(0, len(self.spans) - 1, 2)]
+        if not per:
+            return None
+        per.sort()
+        return per[len(per) // 2]
 
 
 def pmc_traffic():
@@ -296,14 +313,15 @@ def main():
     if dp:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss, probs = trainer.step(x, y, tok)
-    torch.cuda.synchronize()
-    if dp:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    with TowerTimer(trainer.img) as tt:
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss, probs = trainer.step(x, y, tok)
+        torch.cuda.synchronize()
+        if dp:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
     t = torch.tensor([dt], device=dev)
     if dp:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -316,9 +334,13 @@ def main():
     with GemmTimer(ops) as gt:
         trainer.eager_step(x, y, tok)
     gs = gt.summary()
-    with TowerTimer(trainer.img) as tt:
-        trainer.eager_step(x, y, tok)
     img_ms = tt.ms()
+    img_src = "timed loop"
+    if img_ms is None:  # graph replay: the tower's methods are not called per step
+        with TowerTimer(trainer.img) as tt2:
+            trainer.eager_step(x, y, tok)
+            trainer.eager_step(x, y, tok)
+        img_ms, img_src = tt2.ms(), "eager steps after the timed loop (graph mode)"
     tf_stats = time_train_transform(B, dev)
 
     if rank == 0:
@@ -354,9 +376,14 @@ def main():
             "image_tower": {"ms_fwd_bwd": round(img_ms, 3),
                             "tflops": round(B * f_img / (img_ms * 1e-3) / 1e12, 1),
                             "mfma_frac": round(B * f_img / (img_ms * 1e-3) / PEAK_BF16, 4),
+                            "mfma_frac_step_bound": round(B * f_img / (ms * 1e-3) / PEAK_BF16, 4),
                             "flops_per_image": f_img,
+                            "source": img_src,
                             "note": "SURVEY 8(d) north-star ratio: B*F_img / (t_image_tower * "
-                                    "peak), HIP events around the tower's fwd and bwd"},
+                                    "peak), t = median over the timed steps of the HIP-event "
+                                    "spans around the tower's fwd and bwd on the main stream; "
+                                    "mfma_frac_step_bound = the same with the whole step time "
+                                    "(a lower bound of mfma_frac)"},
             "roofline": {"bound": "mfma",
                          "kernel": "gemm8_kernel<EPI 0|2|6, bf16> (256x256 phase-interleaved "
                                    "bf16 MFMA GEMM: QKV, out-proj, c_fc+QuickGELU+QuickGELU', "
@@ -370,7 +397,13 @@ def main():
                          "flops_per_launch": round(gs["pp_flops"] / n_pp),
                          "launches_per_step": gs["pp_n"],
                          "avg_launch_ms": round(gs["pp_ms"] / n_pp, 4),
-                         "all_gemm_share_of_step": round(gs["ms"] / ms, 3)},
+                         "main_stream_gemm_share_of_step": round(gs["ms"] / ms, 3),
+                         "side_stream_gemm_ms": round(gs["side_ms"], 3),
+                         "note": "launches of the dominant kernel on the main (image-chain) "
+                                 "stream, timed with HIP events around each launch of one extra "
+                                 "eager step"},
+            "runtime": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
+                        "side_streams": 1 if trainer._merge_side_streams() else 2},
             "train_transform": tf_stats,
         }
         if world == 1 and not args.no_cpu_baseline:

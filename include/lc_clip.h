@@ -205,10 +205,17 @@ int lc_train_transform(hipStream_t stream, int n, int C, int Hin, int Win, const
  * codes[i] in 0..9 (invert, brightness, color, contrast, sharpness blends, posterize, solarize,
  * autocontrast, equalize, nearest affine) with 6 f32 parameters each in params (the host computes
  * blend ratios, masks, thresholds and the rescaled inverse affine grid matrix, lcclip/transforms.py).
- * C*H*W <= 12288 (CIFAR 32x32, TinyImageNet 64x64). Replaces: transforms.AutoAugment(policy)
+ * C*H*W <= 12288 (CIFAR 32x32, TinyImageNet 64x64; larger: lc_autoaugment_ws). Replaces: transforms.AutoAugment(policy)
  * (methods/_trainer.py:217-228). */
 int lc_autoaugment(hipStream_t stream, int n, int C, int H, int W, const float* x, float* out,
                    int n_ops, const int* codes, const float* params);
+
+/* lc_autoaugment for any image size: images with C*H*W > 12288 (ImageNet / ImageNet-R at
+ * 224x224, the policy methods/_trainer.py:222-224 selects) keep their working image in `out`
+ * and a scratch image in the caller's workspace ws (ws_bytes >= n*C*H*W*4); smaller ones ignore
+ * ws and run the LDS form. Bit-identical results to lc_autoaugment where both apply. */
+int lc_autoaugment_ws(hipStream_t stream, int n, int C, int H, int W, const float* x, float* out,
+                      int n_ops, const int* codes, const float* params, void* ws, long ws_bytes);
 
 /* f32 -> bf16 cast of n elements (weight staging). */
 int lc_cast_bf16(hipStream_t stream, long n, const float* src, void* dst);

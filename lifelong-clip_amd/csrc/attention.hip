@@ -523,15 +523,15 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
 #pragma unroll
       for (int b = 0; b < 2; ++b) {  // 32-column scale blocks: dt = 2b, 2b + 1
         float v[8];
-        float amax = 0.f;
+        uint32_t amax = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           v[i] = bf2f(f2bf(x[2 * b + (i >> 2)][i & 3] * mul));
-          amax = fmaxf(amax, fabsf(v[i]));
+          amax = lc_amax_bits(amax, v[i]);
         }
-        amax = fmaxf(amax, __shfl_xor(amax, 16));
-        amax = fmaxf(amax, __shfl_xor(amax, 32));
-        const uint32_t byte = e8m0_of(amax);
+        amax = max(amax, (uint32_t)__shfl_xor((int)amax, 16));
+        amax = max(amax, (uint32_t)__shfl_xor((int)amax, 32));
+        const uint32_t byte = e8m0_of_bits(amax);
         const float inv = e8m0_inv(byte);
 #pragma unroll
         for (int j = 0; j < 2; ++j)

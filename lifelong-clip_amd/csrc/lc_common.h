@@ -128,26 +128,42 @@ struct Fp8Scales {
 
 // E8M0 block scale of a 32-element block with max |x| = amax (OCP MX: 2^(floor(log2 amax) - 8),
 // e4m3's largest power being 2^8), clamped to [2^-126, 2^126]; amax = 0 (or below the f32 normal
-// range) -> byte 0, every element encodes to 0.
-LC_DEV uint32_t e8m0_of(float amax) {
-  const int e = (int)((__float_as_uint(amax) >> 23) & 0xff);
+// range) -> byte 0, every element encodes to 0. A block holding a NaN or an infinity gets the MX
+// NaN scale 0xFF and NaN codes (pack4_fp8), so a non-finite input stays non-finite through the
+// fp8 GEMM: amax is reduced as the bit pattern of |x| (lc_amax_bits), where NaN and inf order
+// above every finite value (fmaxf would drop the NaN).
+LC_DEV uint32_t lc_amax_bits(uint32_t acc, float x) {
+  const uint32_t b = __float_as_uint(x) & 0x7fffffffu;
+  return acc > b ? acc : b;
+}
+LC_DEV uint32_t e8m0_of_bits(uint32_t amax_bits) {
+  const int e = (int)(amax_bits >> 23);  // sign already cleared
   if (e == 0) return 0;
+  if (e == 255) return 0xFF;  // NaN / inf in the block
   const int b = e - 8;
   return (uint32_t)(b < 1 ? 1 : (b > 253 ? 253 : b));
 }
-// 2^-(byte - 127) as f32 (the multiplier that maps a block into e4m3 range); byte 0 -> 0
+LC_DEV uint32_t e8m0_of(float amax) { return e8m0_of_bits(__float_as_uint(amax) & 0x7fffffffu); }
+// 2^-(byte - 127) as f32 (the multiplier that maps a block into e4m3 range); byte 0 -> 0,
+// byte 0xFF (NaN scale) -> NaN
 LC_DEV float e8m0_inv(uint32_t byte) {
   if (byte == 0) return 0.f;
+  if (byte == 0xFF) return __uint_as_float(0x7fc00000u);
   return __uint_as_float((uint32_t)(254 - byte) << 23);
 }
-// four f32 -> four e4m3fn bytes (RNE), saturated to +-448 first
+// four f32 -> four e4m3fn bytes (RNE), saturated to +-448 first. The four values come from one
+// scale block, so they are NaN together (NaN scale) or finite together: a NaN group encodes as
+// the e4m3fn NaN code 0x7F (the clamp alone would turn NaN into -448).
 LC_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
+  // integer test: attention.o is built with -fno-honor-nans, where a != a folds to false
+  const bool nan = (__float_as_uint(a) & 0x7fffffffu) > 0x7f800000u;
   a = fminf(fmaxf(a, -448.f), 448.f);
   b = fminf(fmaxf(b, -448.f), 448.f);
   c = fminf(fmaxf(c, -448.f), 448.f);
   d = fminf(fmaxf(d, -448.f), 448.f);
   uint32_t r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  return nan ? 0x7f7f7f7fu : r;
 }
 
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).

@@ -76,16 +76,16 @@ LC_DEV void store_row_fp8(uint8_t* __restrict__ p, uint8_t* __restrict__ scales,
 #pragma unroll
   for (int i = 0; i < V / 4; ++i) {
     float q[4];
-    float amax = 0.f;
+    uint32_t amax = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       q[j] = bf2f(f2bf(v[4 * i + j]));
-      amax = fmaxf(amax, fabsf(q[j]));
+      amax = lc_amax_bits(amax, q[j]);
     }
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    amax = fmaxf(amax, __shfl_xor(amax, 4));
-    const uint32_t byte = e8m0_of(amax);
+    amax = max(amax, (uint32_t)__shfl_xor((int)amax, 1));
+    amax = max(amax, (uint32_t)__shfl_xor((int)amax, 2));
+    amax = max(amax, (uint32_t)__shfl_xor((int)amax, 4));
+    const uint32_t byte = e8m0_of_bits(amax);
     const float inv = e8m0_inv(byte);
     const int k = i * 256 + lane * 4;
     *reinterpret_cast<uint32_t*>(p + k) = pack4_fp8(q[0] * inv, q[1] * inv, q[2] * inv, q[3] * inv);

@@ -43,12 +43,12 @@ quant_fp8_kernel(long rows, int K, const void* __restrict__ src, int src_f32, lo
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = 0.f;
     }
-    float amax = 0.f;
+    uint32_t amax = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) amax = fmaxf(amax, fabsf(v[i]));
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    const uint32_t byte = e8m0_of(amax);
+    for (int i = 0; i < 8; ++i) amax = lc_amax_bits(amax, v[i]);
+    amax = max(amax, (uint32_t)__shfl_xor((int)amax, 1));
+    amax = max(amax, (uint32_t)__shfl_xor((int)amax, 2));
+    const uint32_t byte = e8m0_of_bits(amax);
     const float inv = e8m0_inv(byte);
     if (on) {
       uint2 q;

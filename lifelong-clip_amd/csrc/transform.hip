@@ -362,13 +362,28 @@ LC_DEV int gray_u8(int r, int g, int b) {  // rgb_to_grayscale(uint8): (0.2989r 
   return (int)s;
 }
 
+// GLB = false: both working images in LDS (C*H*W <= 12288). GLB = true (larger images, e.g.
+// ImageNet-R at 3 x 224 x 224): the current image lives in this image's slice of `out` (as ints,
+// converted to f32 in place at the end) and the scratch image in the caller's workspace `ws`;
+// the histogram / reductions stay in LDS. Same arithmetic in the same order either way: the two
+// forms are bit-identical (tests/test_autoaug_gpu.py).
+template <bool GLB>
 __global__ void __launch_bounds__(256)
-autoaug_kernel(int C, int H, int W, const float* __restrict__ x, float* __restrict__ out, AugOps ops) {
+autoaug_kernel(int C, int H, int W, const float* __restrict__ x, float* out, AugOps ops, int* ws) {
   extern __shared__ int sm[];
   const int HW = H * W, tot = C * HW;
-  int* a = sm;                 // current image
-  int* b = sm + tot;           // scratch image
-  int* hist = b + tot;         // [C][256] histogram / LUT
+  int* a;     // current image
+  int* b;     // scratch image
+  int* hist;  // [C][256] histogram / LUT
+  if constexpr (GLB) {
+    a = reinterpret_cast<int*>(out) + (long)blockIdx.x * tot;
+    b = ws + (long)blockIdx.x * tot;
+    hist = sm;
+  } else {
+    a = sm;
+    b = sm + tot;
+    hist = b + tot;
+  }
   int* red = hist + 4 * 256;   // reductions: [0..3] min, [4..7] max, [8] gray sum
   const int tid = threadIdx.x;
   const float* src = x + (long)blockIdx.x * tot;
@@ -514,18 +529,26 @@ autoaug_kernel(int C, int H, int W, const float* __restrict__ x, float* __restri
     __syncthreads();
   }
   float* dst = out + (long)blockIdx.x * tot;
-  for (int k = tid; k < tot; k += blockDim.x) dst[k] = (float)a[k] / 255.0f;  // .float() / 255
+  // .float() / 255 (GLB: a may be dst itself; each lane converts the elements it reads)
+  for (int k = tid; k < tot; k += blockDim.x) dst[k] = (float)a[k] / 255.0f;
 }
 
 }  // namespace
 
 extern "C" {
 
-int lc_autoaugment(hipStream_t st, int n, int C, int H, int W, const float* x, float* out,
-                   int n_ops, const int* codes, const float* params) {
-  LC_CHECK_ARG(n > 0 && C >= 1 && C <= 4 && H > 0 && W > 0 && C * H * W <= 12288);
+// Images larger than the LDS form (C*H*W > 12288) need ws: n * C*H*W ints (lc_autoaugment_ws)
+static int autoaug_launch(hipStream_t st, int n, int C, int H, int W, const float* x, float* out,
+                          int n_ops, const int* codes, const float* params, void* ws,
+                          long ws_bytes) {
+  LC_CHECK_ARG(n > 0 && C >= 1 && C <= 4 && H > 0 && W > 0);
   LC_CHECK_ARG(n_ops >= 0 && n_ops <= 2 && x != nullptr && out != nullptr);
   LC_CHECK_ARG(n_ops == 0 || (codes != nullptr && params != nullptr));
+  const long tot = (long)C * H * W;
+  const bool glb = tot > 12288;
+  LC_CHECK_ARG(tot <= (1L << 30) / n);
+  LC_CHECK_ARG(!glb || (ws != nullptr && ws_bytes >= (long)n * tot * (long)sizeof(int) &&
+                        (reinterpret_cast<uintptr_t>(out) & 3) == 0));
   AugOps ops{};
   ops.n = n_ops;
   for (int o = 0; o < n_ops; ++o) {
@@ -534,9 +557,27 @@ int lc_autoaugment(hipStream_t st, int n, int C, int H, int W, const float* x, f
     ops.code[o] = codes[o];
     for (int k = 0; k < 6; ++k) ops.p[o][k] = params[o * 6 + k];
   }
-  const size_t shm = (size_t)(2 * C * H * W + 4 * 256 + 16) * sizeof(int);
-  hipLaunchKernelGGL(autoaug_kernel, dim3(n), dim3(256), shm, st, C, H, W, x, out, ops);
+  if (glb) {
+    const size_t shm = (size_t)(4 * 256 + 16) * sizeof(int);
+    hipLaunchKernelGGL(autoaug_kernel<true>, dim3(n), dim3(256), shm, st, C, H, W, x, out, ops,
+                       static_cast<int*>(ws));
+  } else {
+    const size_t shm = (size_t)(2 * tot + 4 * 256 + 16) * sizeof(int);
+    hipLaunchKernelGGL(autoaug_kernel<false>, dim3(n), dim3(256), shm, st, C, H, W, x, out, ops,
+                       nullptr);
+  }
   LC_LAUNCH_RET();
+}
+
+int lc_autoaugment(hipStream_t st, int n, int C, int H, int W, const float* x, float* out,
+                   int n_ops, const int* codes, const float* params) {
+  LC_CHECK_ARG((long)C * H * W <= 12288);  // larger images: lc_autoaugment_ws
+  return autoaug_launch(st, n, C, H, W, x, out, n_ops, codes, params, nullptr, 0);
+}
+
+int lc_autoaugment_ws(hipStream_t st, int n, int C, int H, int W, const float* x, float* out,
+                      int n_ops, const int* codes, const float* params, void* ws, long ws_bytes) {
+  return autoaug_launch(st, n, C, H, W, x, out, n_ops, codes, params, ws, ws_bytes);
 }
 
 }  // extern "C"

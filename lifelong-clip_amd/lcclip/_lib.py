@@ -45,6 +45,7 @@ SIGNATURES = {
     "lc_train_transform": [P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, P,
                            P, c_int, c_int, c_int, P],
     "lc_autoaugment": [P, c_int, c_int, c_int, c_int, P, P, c_int, P, P],
+    "lc_autoaugment_ws": [P, c_int, c_int, c_int, c_int, P, P, c_int, P, P, P, c_long],
     "lc_cast_bf16": [P, c_long, P, P],
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_cast_weights_bf16": [P, c_int, P, P, P, P, P],

@@ -62,6 +62,7 @@ class StagedBlock:
     def __init__(self):
         self.frozen_key = None
         self.peft_key = None
+        self.merge_epoch = 0  # advanced on every LoRA re-merge (part of the fp8 staging key)
 
 
 class BlockStack:
@@ -136,6 +137,9 @@ class BlockStack:
                     st.lora_out = self._stage_lora(st, "lora_out", attn.out_proj.lora_A,
                                                    attn.out_proj.lora_B)
                     st.peft_key = pkey
+                    # the fused AdamW bypasses the version counters, so the re-merged weights can
+                    # carry the same pkey as before: the epoch is what tells _stage_fp8 to re-quantise
+                    st.merge_epoch += 1
             elif self.variant == "adapter":
                 ad = blk.adaptmlp
                 pkey = _key(ad.down_proj.weight, ad.up_proj.weight)
@@ -165,7 +169,7 @@ class BlockStack:
             if D % 256:
                 raise ValueError(f"precision='fp8' needs a width that is a multiple of 256 (got {D}): "
                                  "the fp8 GEMM tiles N in 256-column blocks")
-            key = (st.frozen_key, st.peft_key)
+            key = (st.frozen_key, st.peft_key, st.merge_epoch)
             if getattr(st, "q_key", None) == key:
                 continue
             attn, mlp = blk.attn, blk.mlp

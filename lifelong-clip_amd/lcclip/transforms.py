@@ -211,6 +211,9 @@ def _affine_grid_theta(m, width, height):
             float(t[3] / sy), float(t[4] / sy), float(t[5] / sy)]
 
 
+# largest C*H*W whose two working images fit the LDS form of lc_autoaugment (transform.hip)
+AUTOAUG_LDS_ELEMS = 12288
+
 # lc_autoaugment op codes (transform.hip AA_*)
 _AA = {"Invert": 0, "Brightness": 1, "Color": 2, "Contrast": 3, "Sharpness": 4, "Posterize": 5,
        "Solarize": 6, "AutoContrast": 7, "Equalize": 8}
@@ -272,8 +275,14 @@ def autoaugment(x, ops):
     out = torch.empty_like(x)
     cb = (ctypes.c_int * max(len(codes), 1))(*codes)
     pb = (ctypes.c_float * max(len(params), 1))(*params)
-    call("lc_autoaugment", stream_of(x), n, C, H, W, ptr(x), ptr(out), len(codes),
-         ctypes.cast(cb, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p))
+    if C * H * W <= AUTOAUG_LDS_ELEMS:  # the image fits the kernel's LDS form
+        call("lc_autoaugment", stream_of(x), n, C, H, W, ptr(x), ptr(out), len(codes),
+             ctypes.cast(cb, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p))
+    else:  # ImageNet-sized: working images in HBM (out + a scratch image per input)
+        ws = torch.empty(n * C * H * W, dtype=torch.int32, device=x.device)
+        call("lc_autoaugment_ws", stream_of(x), n, C, H, W, ptr(x), ptr(out), len(codes),
+             ctypes.cast(cb, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p), ptr(ws),
+             ws.numel() * 4)
     return out
 
 

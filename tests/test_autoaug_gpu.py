@@ -76,3 +76,38 @@ def test_train_transform_with_autoaugment(dev):
         pref = o.patchify(ref, 16)
         assert ((pt.float().cpu() - pref).abs() <= pref.abs() * 2 ** -7 + 1e-6).all()
     assert n_aug >= 3
+
+
+@pytest.mark.parametrize("op", OPS)
+def test_autoaug_op_bitexact_large_image(dev, op):
+    """Images larger than the LDS form (ImageNet-R's 3 x 224 x 224; also a ragged 3 x 72 x 90)
+    go through lc_autoaugment_ws (working image in HBM) with the same arithmetic: bit-exact vs
+    the oracle for every op (these used to be rejected by the kernel)."""
+    from lcclip.transforms import augmentation_space, autoaugment
+    for (H, W) in ((224, 224), (72, 90)):
+        x = images(2, H, W, seed=len(op) + W)
+        mags, signed = augmentation_space(10, H, W)[op]
+        b = 7 if mags.dim() else None
+        base = float(mags[b].item()) if b is not None else 0.0
+        for sgn in ((1, -1) if signed else (1,)):
+            ops = [(op, base * sgn)]
+            got = autoaugment(x.to(dev), ops).cpu()
+            ref = o.autoaugment(x, ops)
+            assert torch.equal(got, ref), (op, H, W, sgn, (got - ref).abs().max().item())
+
+
+def test_train_transform_imagenet_r_draws(dev):
+    """TrainTransform.for_dataset('imagenet-r') on a 3 x 224 x 224 batch: the ImageNet policy's
+    drawn sub-policies (an active op in most draws) run through the whole transform without
+    error and match the oracle (the r2 kernel raised LcError on the first active op)."""
+    from lcclip.transforms import TrainTransform
+    tf = TrainTransform.for_dataset("imagenet-r", generator=torch.Generator().manual_seed(4))
+    x = images(3, 224, 224, seed=21)
+    n_aug = 0
+    for _ in range(5):
+        ops, i, j, flip = tf.draw(224, 224)
+        n_aug += bool(ops)
+        ref = o.train_transform(x, 224, 4, i, j, flip, tf.mean, tf.std, aug_ops=ops)
+        got = tf(x.to(dev), params=(ops, i, j, flip))
+        assert (got.cpu() - ref).abs().max().item() < 2e-6, ops
+    assert n_aug >= 2

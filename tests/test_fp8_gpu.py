@@ -200,3 +200,65 @@ def test_attn_bwd_fp8_matches_quant(ops, dev, n_seq, L, H, causal):
     q = ops.attn_bwd_fp8(qkv, O, dO, lse, ops.Fp8Mat(M, 3 * D, dev), n_seq, L, H, causal)
     assert torch.equal(q.data, ref.data)
     assert torch.equal(gpu_scales(q), gpu_scales(ref))
+
+
+def test_lora_fp8_weights_requantised_after_step(dev, ops):
+    """LoRA + precision='fp8': the fused AdamW writes the LoRA parameters through the C ABI (no
+    torch version bump), so after an optimizer step the re-merged QKV weight must be quantised
+    again — the staged fp8 image equals quant_fp8 of the current bf16 merge, not of the old one
+    (the fp8 key used to stay equal across the re-merge)."""
+    from lcclip import OnlineTrainer
+    from lcclip.adapter_clip import AdapterCLIP
+    cfg = o.TINY_MAPLE8  # vision width 256: the fp8 tiles cover it
+    sd = o.synthetic_state_dict(cfg, "lora", "both", seed=17)
+    w = AdapterCLIP.from_state_dict(sd, "lora", "both", device=dev)
+    stack = w.model.visual.transformer.engine
+    stack.precision = "fp8"
+    tr = OnlineTrainer(w, lr=5e-2)
+    img = o.synthetic_images(4, cfg.image_resolution, seed=3).to(dev)
+    tok = o.synthetic_tokens(3, 77, seed=3, vocab=cfg.vocab_size).to(dev)
+    y = torch.tensor([0, 1, 2, 1], device=dev)
+    tr.step(img, y, tok)
+    st = stack.staged[0]
+    before = st.q["wqkv"].data.clone()
+    tr.step(img, y, tok)  # the second step's forward stages the weights AdamW moved in step 1
+    torch.cuda.synchronize()
+    want = ops.quant_fp8(st.wqkv)
+    assert torch.equal(st.q["wqkv"].data, want.data)
+    assert torch.equal(st.q["wqkv"].scales, want.scales)
+    assert not torch.equal(before, want.data), "the LoRA update did not move the merged weight"
+
+
+def test_fp8_keeps_non_finite(ops, dev):
+    """A NaN or an infinity in a 32-block is not laundered into finite codes: the
+    block gets the MX NaN scale byte 0xFF and the e4m3fn NaN code 0x7F, finite blocks are
+    unchanged, and the fp8 GEMM / the MUL_Q8 epilogue carry the non-finite value on to their
+    outputs (the trainer's non-finite check then skips the update)."""
+    M, N, K = 300, 256, 256
+    g = torch.Generator(device=dev).manual_seed(5)
+    A = torch.randn(M, K, device=dev, generator=g)
+    Ab = A.clone()
+    Ab[3, 40] = float("nan")   # row 3, block 1
+    Ab[7, 200] = float("inf")  # row 7, block 6
+    Ab[9, 0] = -float("inf")   # row 9, block 0
+    q, ref = ops.quant_fp8(Ab), ops.quant_fp8(A)
+    s, sref = gpu_scales(q).view(torch.uint8), gpu_scales(ref).view(torch.uint8)
+    bad = {(3, 1), (7, 6), (9, 0)}
+    for r, b in bad:
+        assert s[r, b].item() == 0xFF
+        assert (q.data[r, 32 * b:32 * b + 32].view(torch.uint8) & 0x7F == 0x7F).all()
+    keep = torch.ones_like(s, dtype=torch.bool)
+    for r, b in bad:
+        keep[r, b] = False
+    assert torch.equal(s[keep], sref[keep])
+    B = torch.randn(N, K, device=dev, generator=g) * K ** -0.5
+    out = torch.empty(M, N, device=dev)
+    ops.gemm_nt_fp8(q, ops.quant_fp8(B), ops.EPI_F32, out)
+    assert not torch.isfinite(out[[3, 7, 9]]).any(dim=1).any()
+    assert torch.isfinite(out[[0, 1, 2, 4, 5, 6, 8]]).all()
+    aux = torch.randn(M, N, device=dev, generator=g).to(BF)
+    aux[11, 70] = float("nan")
+    qo = ops.gemm_nt_fp8(ops.quant_fp8(A), ops.quant_fp8(B), ops.EPI_MUL_Q8, None, aux=aux,
+                         q_out=ops.Fp8Mat(M, N, dev))
+    assert gpu_scales(qo).view(torch.uint8)[11, 2].item() == 0xFF
+    assert gpu_scales(qo).view(torch.uint8)[12, 2].item() != 0xFF

@@ -213,11 +213,14 @@ def _step_vs_oracle(dev, method, B, C, seed, tag):
     cos_o = {n: cs(g16[n], g32[n]) for n in g32}
     cat = lambda d: torch.cat([d[n].flatten() for n in g32])  # noqa: E731
     flat, flat_o = rel(cat(gg), cat(g32)), rel(cat(g16), cat(g32))
+    flat_b = rel(cat(gg), cat(g16))  # vs the bf16-rounding oracle: the implementation's fidelity
+    cos_b = {n: cs(gg[n], g16[n]) for n in g32}
     m = dict(probs_abs_vs_fp32=(probs.cpu() - p32).abs().max().item(),
              loss_abs=abs(loss.item() - loss32.item()), grad_flat_rel_vs_fp32=flat,
              grad_rel_max_vs_fp32=max(e32.values()), grad_cos_min=min(cos.values()),
              oracle_bf16_grad_flat_rel=flat_o, oracle_bf16_grad_rel_max=max(eo.values()),
              oracle_bf16_grad_cos_min=min(cos_o.values()), n_grads=len(e32),
+             grad_flat_rel_vs_bf16_oracle=flat_b, grad_cos_min_vs_bf16_oracle=min(cos_b.values()),
              **logit_metrics(ls * fi.cpu() @ ft.cpu().t(), ls * i32 @ t32.t(), None, ls))
     record(test=tag, method=method, B=B, C=C, **m)
     assert m["probs_abs_vs_fp32"] < 1e-2 and m["loss_abs"] < 1e-2, m

@@ -282,3 +282,21 @@ def test_autoaugment_draw_sequence():
     assert (i, j) == (int(torch.randint(0, 9, (1,), generator=g)),
                       int(torch.randint(0, 9, (1,), generator=g)))
     assert flip == bool(torch.rand(1, generator=g) < 0.5)
+
+
+def test_autoaugment_policies_match_reference_tables():
+    """AUTOAUG_POLICIES (op, probability, magnitude bin) equals the sub-policy tables the
+    reference holds in its own tree (utils/augment.py:24-163: ImageNet / CIFAR10 / SVHN, parsed
+    as text into tests/golden/autoaug_policies_ref.json by tests/golden/make_autoaug_golden.py;
+    this test needs no /root/reference). The reference trains with torchvision's AutoAugment
+    (methods/_trainer.py:217-228), whose tables are the same published policies."""
+    import json
+    from lcclip.transforms import AUTOAUG_POLICIES
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                      "autoaug_policies_ref.json")))["policies"]
+    assert sorted(ref) == sorted(AUTOAUG_POLICIES)
+    for name, rows in ref.items():
+        mine = [[[op, p, b] for (op, p, b) in row] for row in AUTOAUG_POLICIES[name]]
+        assert len(mine) == len(rows) == 25
+        for i, (a, b) in enumerate(zip(mine, rows)):
+            assert a == b, (name, i, a, b)
