@@ -242,6 +242,18 @@ int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY,
                  const void* X, long ldx, const float* A, const float* B, float scaling,
                  float* dA, float* dB);
 
+/* The same gradients in ONE pass over X [M,K] and dY [M,N] (bf16), MFMA form: apad = A as bf16
+ * [>= 16 rows, K] and btpad = B^T as bf16 [>= 16 rows, N], rows >= r zero (the engine stages
+ * both per step); dA [r,K] / dB [N,r] f32 accumulated (+=). 32-row blocks, one persistent
+ * workgroup per CU, partial sums in ws after its first LC_SPLITK_TICKET_BYTES (needs
+ * walkers x (16 N + 16 K) x 4 B, walkers = min(CUs, ceil(M/32))) summed by a second launch in
+ * walker order (deterministic). Shapes: (K, N) in {(768, 2304), (768, 768), (512, 1536),
+ * (512, 512)} (ViT-B/16 image / text QKV and out-proj sites); r <= 16.
+ * Replaces: autograd of the two F.linear LoRA products (lora.py:838-839, 1073-1074). */
+int lc_lora_grad_ws(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
+                    const void* X, long ldx, const void* apad, long lda, const void* btpad,
+                    long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes);
+
 /* xout = resid + z + scale*(drop(relu(z Wd^T + bd)) Wu^T + bu); h (bf16 [M,64]) is saved.
  * keep = 1 - dropout p; the counter-based dropout mask is selected by
  * seed + (*seed_dev) * const when seed_dev != NULL (a device-side RNG epoch, so a captured HIP

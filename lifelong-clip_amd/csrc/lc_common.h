@@ -166,6 +166,30 @@ LC_DEV uint32_t pack4_fp8(float a, float b, float c, float d) {
   return nan ? 0x7f7f7f7fu : r;
 }
 
+// LDS images are XOR-swizzled in 32-B units so that the 8 rows {0..3, 8..11} (+16) one
+// ds_read_b64_tr_b16 pass of 32 lanes touches land in 8 distinct 32-B bank groups.
+//   W rows (256 or 512 B): unit u of row r at u ^ ((r & 3) | ((r >> 1) & 4)) (low 3 bits: a
+//     row's bank offset only depends on u mod 8 for both widths)
+//   S rows (128 B = 4 units; two rows per 256-B bank span): unit u at u ^ (((r >> 1) & 1) | ((r >> 2) & 2))
+LC_DEV int swz_w(int r) { return (r & 3) | ((r >> 1) & 4); }
+LC_DEV int swz_s(int r) { return ((r >> 1) & 1) | ((r >> 2) & 2); }
+
+// 8 consecutive k-rows (row, row + 4 of the lane's 4-row group) of one 16-column block, as an
+// MFMA operand: lane (g, t) gets column col0 + t, k = 8g .. 8g+7 of the 32-row k-slice.
+template <int ROWB>
+LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
+  auto addr = [&](int r) {
+    const int byte = col * 2;  // within the row
+    const int u = (byte >> 5) ^ (ROWB >= 256 ? swz_w(r) : swz_s(r));
+    return lds + r * ROWB + u * 32 + (byte & 31);
+  };
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) bf16x4*)addr(row));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) bf16x4*)addr(row + 4));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).
 int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,

@@ -512,6 +512,256 @@ int grid_for(long work, int block) {
   return (int)(gsz < 1 ? 1 : gsz);
 }
 
+// ---------------------------------------------------------------- LoRA gradients, one pass
+// Rank-r (r <= 16) LoRA gradients of one projection site (lora.py:838-839 / 1073-1074 autograd):
+//   XA = X A^T [M, r],  dYB = dY B [M, r],  dB[N, r] += s dY^T XA,  dA[r, K] += s dYB^T X
+// reading X [M, K] and dY [M, N] ONCE (the four-GEMM form streams each of them twice). Rows are
+// independent, so a 32-row block b needs only its own rows: X_b (32 x K, whole, in LDS) gives
+// XA_b; dY_b streams through a 3-slot ring in 128-column chunks, each chunk feeding both dYB_b
+// (row reads) and dB (transposed reads, with XA_b as the other operand); once dY_b has passed,
+// dA += dYB_b^T X_b (transposed reads of X_b). MFMA 16x16x32 with r padded to 16 (A / B^T staged
+// as bf16 [>= 16, K] / [>= 16, N] with zero rows >= r).
+// One persistent workgroup (8 waves) per CU walks row blocks cidx, cidx + walkers, ...; X of
+// the next block and the ring's next chunks are in flight while the current block computes.
+// dB (waves own one 16-column tile of every chunk) and dA (waves own KT/8... column tiles) stay
+// in registers; each walker writes its partial to a workspace slot and lora_reduce_kernel sums
+// the slots in walker order (deterministic, no atomics).
+// Reductions across waves (XA_b: each wave a third of K; dYB_b: each wave one k-step of every
+// chunk) go through LDS. Rows >= M are loaded clamped and their XA / dYB rows set to zero.
+template <int KT, int NC>
+struct LoraGeom {
+  static constexpr int K = KT * 32;
+  static constexpr int XROW = K * 2;              // X image row bytes
+  static constexpr int XIMG = 32 * XROW;          // one X block
+  static constexpr int CHUNK = 32 * 256;          // 32 rows x 128 cols of dY
+  static constexpr int XPIECES = XIMG / 1024 / 8; // X DMA pieces per wave
+  static constexpr int RED = 8 * 32 * 16 * 4;     // per-wave [32][16] f32 partials
+  static constexpr int X_OFF = 0;
+  static constexpr int RING_OFF = 2 * XIMG;
+  static constexpr int RED_OFF = RING_OFF + 3 * CHUNK;
+  static constexpr int XAT_OFF = RED_OFF + RED;   // bf16 [16][32]
+  static constexpr int DYBT_OFF = XAT_OFF + 1024;
+  static constexpr int BYTES = DYBT_OFF + 1024;
+  static constexpr int XKS = KT / 8;              // XA k-steps per wave
+  static constexpr int DAT = KT * 2 / 8;          // dA 16-column tiles per wave
+  static constexpr int SLOT_FLOATS = NC * 128 * 16 + 16 * K;  // dB [N][16] + dA [16][K]
+};
+
+LC_DEV void vm_wait_n(int n) {
+  switch (n) {
+#define LC_VM(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    LC_VM(0) LC_VM(1) LC_VM(2) LC_VM(3) LC_VM(4) LC_VM(5) LC_VM(6) LC_VM(7) LC_VM(8)
+    LC_VM(9) LC_VM(10) LC_VM(11) LC_VM(12) LC_VM(13) LC_VM(14)
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+#undef LC_VM
+  }
+}
+
+template <int KT, int NC>
+__global__ void __launch_bounds__(512, 1)
+lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ dY,
+                   long ldy, const bf16_t* __restrict__ apad, long lda,
+                   const bf16_t* __restrict__ btpad, long ldbt, float* __restrict__ part,
+                   int walkers) {
+  using G = LoraGeom<KT, NC>;
+  constexpr int K = G::K, XROW = G::XROW;
+  __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, t = lane & 15;
+  const int nblk = (M + 31) / 32;
+  const int cidx = blockIdx.x;
+  const int nb = cidx < nblk ? (nblk - 1 - cidx) / walkers + 1 : 0;  // blocks of this walker
+  auto blk_row = [&](int i) { return (cidx + i * walkers) * 32; };
+
+  // DMA: X block i into buffer i & 1 (XPIECES 1-KiB pieces per wave), dY chunk (i, c) into ring
+  // slot q (one piece per wave). Lane -> (row, 16-B position) inverts the 32-B unit swizzle.
+  auto dma_x = [&](int i) {
+    char* dst = smem + G::X_OFF + (i & 1) * G::XIMG;
+    const int r0 = blk_row(i);
+#pragma unroll
+    for (int pp = 0; pp < G::XPIECES; ++pp) {
+      const int piece = wave * G::XPIECES + pp;
+      const int idx = piece * 64 + lane;          // 16-B position in the image
+      const int row = idx / (XROW / 16), pc = idx % (XROW / 16);
+      const int c = (((pc >> 1) ^ swz_w(row)) << 1) | (pc & 1);
+      const int m = min(r0 + row, M - 1);
+      glds16(X + (long)m * ldx + c * 8, dst + piece * 1024);
+    }
+  };
+  auto dma_c = [&](int i, int c, int q) {
+    char* dst = smem + G::RING_OFF + q * G::CHUNK;
+    const int idx = wave * 64 + lane;
+    const int row = idx >> 4, pc = idx & 15;
+    const int cc = (((pc >> 1) ^ swz_w(row)) << 1) | (pc & 1);
+    const int m = min(blk_row(i) + row, M - 1);
+    glds16(dY + (long)m * ldy + c * 128 + cc * 8, dst + wave * 1024);
+  };
+  // row read (A operand): row `row` (lane t's), 16-B chunk `ch` of an image with ROWB-byte rows
+  auto row_frag = [&](const char* img, int rowb, int row, int ch) {
+    const int u = (ch >> 1) ^ swz_w(row);
+    return *reinterpret_cast<const bf16x8*>(img + row * rowb + u * 32 + (ch & 1) * 16);
+  };
+
+  // per-walker constant fragments: A rows (XA's B operand) for this wave's k-steps, B^T rows
+  // (dYB's B operand) for this wave's k-step of every chunk
+  bf16x8 af[G::XKS], bf[NC];
+  // (inline-asm loads: hipcc would otherwise wait vmcnt(0) — draining the LDS-DMA ring — at
+  // every use inside the loop; the explicit wait below retires them before the first DMA)
+#pragma unroll
+  for (int k = 0; k < G::XKS; ++k)
+    asm volatile("global_load_dwordx4 %0, %1, off"
+                 : "=v"(af[k])
+                 : "v"(apad + (long)t * lda + (wave * G::XKS + k) * 32 + g * 8));
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    asm volatile("global_load_dwordx4 %0, %1, off"
+                 : "=v"(bf[c])
+                 : "v"(btpad + (long)t * ldbt + c * 128 + (wave >> 1) * 32 + g * 8));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // LDS hand-offs between waves with LDS-DMA in flight: a raw barrier behind lgkmcnt(0)
+  // (__syncthreads() would wait vmcnt(0) and drain the ring)
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 accB[NC], accA[G::DAT];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) accB[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < G::DAT; ++j) accA[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* red = reinterpret_cast<float*>(smem + G::RED_OFF);
+  bf16_t* xat = reinterpret_cast<bf16_t*>(smem + G::XAT_OFF);
+  bf16_t* dybt = reinterpret_cast<bf16_t*>(smem + G::DYBT_OFF);
+
+  // issue order per block i: [X_{i+1}], then one chunk piece per chunk step (the ring runs two
+  // chunks ahead, across block seams); prologue: X_0, chunks (0,0), (0,1)
+  if (nb > 0) {
+    dma_x(0);
+    dma_c(0, 0, 0);
+    if (NC > 1) dma_c(0, 1, 1);
+  }
+  int slot = 0;  // ring slot of the current chunk
+  for (int i = 0; i < nb; ++i) {
+    const bool more = i + 1 < nb;
+    // X_i landed: younger ops are the two ring pieces issued after it
+    vm_wait_n(NC > 1 ? 2 : 1);
+    __builtin_amdgcn_s_barrier();
+    const char* ximg = smem + G::X_OFF + (i & 1) * G::XIMG;
+    // ---- XA_i partial: wave's k-steps, both 16-row subtiles
+    {
+      f32x4 xa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k = 0; k < G::XKS; ++k)
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+          xa[sub] = mfma16(row_frag(ximg, XROW, sub * 16 + t, (wave * G::XKS + k) * 4 + g), af[k], xa[sub]);
+      // lane holds XA[m = sub*16 + 4g + rr][r = t]
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[(wave * 32 + sub * 16 + 4 * g + rr) * 16 + t] = xa[sub][rr];
+    }
+    if (more) dma_x(i + 1);  // buffer (i+1)&1 was last read by block i-1's dA (before its end barrier)
+    lds_barrier();
+    {
+      const int m = tid >> 4, r = tid & 15;  // 512 threads = 32 rows x 16
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(w * 32 + m) * 16 + r];
+      xat[r * 32 + m] = f2bf(blk_row(i) + m < M ? v : 0.f);
+    }
+    lds_barrier();
+    const bf16x8 xaf = *reinterpret_cast<const bf16x8*>(xat + t * 32 + g * 8);  // XA[8g..8g+7][t]
+    f32x4 dyb = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int sub = wave & 1, ks = wave >> 1;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      // chunk c landed (younger: the next chunk's piece, and X_{i+1} for c < 2)
+      // ops younger than chunk c: the piece issued at step c - 1 (c == 0: chunk 1, issued one
+      // block earlier or in the prologue) and X_{i+1} (issued after chunks 0 and 1)
+      const int younger = (c == 0 ? (NC > 1 ? 1 : 0) : ((c + 1 < NC || more) ? 1 : 0)) +
+                          (c < 2 && more ? G::XPIECES : 0);
+      vm_wait_n(younger);
+      __builtin_amdgcn_s_barrier();  // also: every wave done with the slot the next DMA reuses
+      // the ring stays two chunks ahead, across the block seam
+      {
+        const int nc = c + 2, nq = slot >= 1 ? slot - 1 : 2;  // slot of chunk c + 2 (== c - 1)
+        if (nc < NC) dma_c(i, nc, nq);
+        else if (more && nc - NC < NC) dma_c(i + 1, nc - NC, nq);
+      }
+      const char* cimg = smem + G::RING_OFF + slot * G::CHUNK;
+      // dYB partial: rows sub*16 + t, k-step ks of this chunk
+      dyb = mfma16(row_frag(cimg, 256, sub * 16 + t, ks * 4 + g), bf[c], dyb);
+      // dB tile `wave` of this chunk: A = dY^T (transposed reads), B = XA
+      accB[c] = mfma16(tr_frag<256>(cimg, 8 * g + (t >> 2), wave * 16 + (t & 3) * 4), xaf, accB[c]);
+      slot = slot == 2 ? 0 : slot + 1;
+    }
+    // ---- dYB_i: sum the 4 waves of each subtile (each did a quarter of the k-steps)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) red[(wave * 32 + sub * 16 + 4 * g + rr) * 16 + t] = dyb[rr];
+    lds_barrier();
+    {
+      const int m = tid >> 4, r = tid & 15, sb = m >> 4;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v += red[((2 * w + sb) * 32 + m) * 16 + r];
+      dybt[r * 32 + m] = f2bf(blk_row(i) + m < M ? v : 0.f);
+    }
+    lds_barrier();
+    // ---- dA += dYB_i^T X_i: A = dYB^T rows, B = X_i columns (transposed reads)
+    const bf16x8 dyf = *reinterpret_cast<const bf16x8*>(dybt + t * 32 + g * 8);
+#pragma unroll
+    for (int j = 0; j < G::DAT; ++j)
+      accA[j] = mfma16(dyf, tr_frag<XROW>(ximg, 8 * g + (t >> 2), (wave * G::DAT + j) * 16 + (t & 3) * 4), accA[j]);
+  }
+  // walker partial: dB [N][16] (lane: rows n = c*128 + wave*16 + 4g + rr, col r = t), dA [16][K]
+  // (lane: rows r = 4g + rr, col k = (wave*DAT + j)*16 + t)
+  float* slot_p = part + (long)cidx * G::SLOT_FLOATS;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      slot_p[(c * 128 + wave * 16 + 4 * g + rr) * 16 + t] = accB[c][rr];
+#pragma unroll
+  for (int j = 0; j < G::DAT; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      slot_p[NC * 128 * 16 + (4 * g + rr) * K + (wave * G::DAT + j) * 16 + t] = accA[j][rr];
+}
+
+// dB[n][j] += s * sum_w part_w dB[n][j],  dA[j][k] += s * sum_w part_w dA[j][k]  (j < r)
+__global__ void __launch_bounds__(256)
+lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats, int N, int K,
+                   int r, float s, float* __restrict__ dA, float* __restrict__ dB) {
+  const int nb = N * r, na = r * K;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nb + na; e += gridDim.x * 256) {
+    long off;
+    float* dst;
+    if (e < nb) {
+      const int n = e / r, j = e % r;
+      off = (long)n * 16 + j;
+      dst = dB + (long)n * r + j;
+    } else {
+      const int j = (e - nb) / K, k = (e - nb) % K;
+      off = (long)N * 16 + (long)j * K + k;
+      dst = dA + (long)j * K + k;
+    }
+    float v = 0.f;
+    int w = 0;
+    for (; w + 8 <= walkers; w += 8) {
+      float q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = part[(long)(w + u) * slot_floats + off];
+      v += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+    }
+    for (; w < walkers; ++w) v += part[(long)w * slot_floats + off];
+    *dst += s * v;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -565,6 +815,41 @@ int lc_lora_grad(hipStream_t st, int M, int N, int K, int r, const void* dY, lon
   else
     hipLaunchKernelGGL((lora_grad_kernel<4, 3072, 1024>), dim3(grid), dim3(256), 0, st, M, N, K,
                        (const bf16_t*)dY, ldy, (const bf16_t*)X, ldx, A, B, scaling, dA, dB);
+  LC_LAUNCH_RET();
+}
+
+int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
+                    const void* X, long ldx, const void* apad, long lda, const void* btpad,
+                    long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes) {
+  LC_CHECK_ARG(M > 0 && r >= 1 && r <= 16 && dY && X && apad && btpad && dA && dB && ws);
+  LC_CHECK_ARG(ldy % 8 == 0 && ldx % 8 == 0 && lda % 8 == 0 && ldbt % 8 == 0);
+  LC_CHECK_ARG(ldy >= N && ldx >= K && lda >= K && ldbt >= N);
+  const int nblk = (M + 31) / 32;
+  int walkers = 0;
+  {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    walkers = nblk < cus ? nblk : cus;
+  }
+  const long slot = (long)N * 16 + 16L * K;
+  LC_CHECK_ARG(ws_bytes >= LC_SPLITK_TICKET_BYTES + (long)walkers * slot * 4);
+  float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
+#define LC_LG(KT, NC)                                                                           \
+  if (K == KT * 32 && N == NC * 128) {                                                         \
+    hipLaunchKernelGGL((lora_grad1p_kernel<KT, NC>), dim3(walkers), dim3(512), 0, st, M,        \
+                       (const bf16_t*)X, ldx, (const bf16_t*)dY, ldy, (const bf16_t*)apad, lda, \
+                       (const bf16_t*)btpad, ldbt, part, walkers);                             \
+  } else
+  LC_LG(24, 18) LC_LG(24, 6) LC_LG(16, 12) LC_LG(16, 4)
+  { return LC_EINVAL; }
+#undef LC_LG
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return LC_ELAUNCH;
+  const int tot = N * r + r * K;
+  hipLaunchKernelGGL(lora_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, part, walkers,
+                     slot, N, K, r, scaling, dA, dB);
   LC_LAUNCH_RET();
 }
 

@@ -50,6 +50,8 @@ SIGNATURES = {
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_cast_weights_bf16": [P, c_int, P, P, P, P, P],
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
+    "lc_lora_grad_ws": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
+                        c_float, P, P, P, c_long],
     "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
                        P, c_long, P],
     "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long],

@@ -512,12 +512,24 @@ class BlockStack:
                               self._grad(grads, ad.down_proj.bias))
         return dz
 
+    # LCCLIP_LORA_1P=0: the four-GEMM form (A/B experiments)
+    LORA_1P = os.environ.get("LCCLIP_LORA_1P", "1") != "0"
+
     def _lora_grad(self, dY, X, A, B, scaling, grads, padded):
-        """Rank-r LoRA gradients (lora.py:838-839, 1073-1074 autograd) as four streaming GEMMs:
-        XA = X A^T and dYB = dY B (skinny, [M,64] bf16 with zero columns >= r), then
+        """Rank-r LoRA gradients (lora.py:838-839, 1073-1074 autograd): one pass over X and dY
+        (ops.lora_grad_1p: XA = X A^T and dYB = dY B per 32-row block, dB += s dY^T XA and
+        dA += s dYB^T X from the same staged rows), or for shapes it does not cover four
+        streaming GEMMs: XA and dYB (skinny, [M,64] bf16 with zero columns >= r), then
         dB += s dY^T XA and dA += s dYB^T X (gemm_tn, outputs masked to r)."""
         a_pad, bt_pad, _ = padded
         M = dY.shape[0]
+        r, K = A.shape
+        N = B.shape[0]
+        if self.LORA_1P and (K, N) in ((768, 2304), (768, 768), (512, 1536), (512, 512)):
+            with self._side():
+                ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, self._grad(grads, A),
+                                 self._grad(grads, B))
+            return
         with self._side():
             xa = _empty((M, 64), BF16, dY.device)
             dyb = _empty((M, 64), BF16, dY.device)

@@ -295,6 +295,24 @@ def lora_grad(dY, X, A, B, scaling, dA, dB):
          X.stride(0), ptr(A), ptr(B), float(scaling), ptr(dA), ptr(dB))
 
 
+def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
+    """dB [N,r] += s dY^T (X A^T), dA [r,K] += s (dY B)^T X in one pass over X and dY
+    (lc_lora_grad_ws); a_pad [>=16, K] / bt_pad [>=16, N] bf16 with rows >= r zero."""
+    _rowmajor(dY, BF16, "dY")
+    _rowmajor(X, BF16, "X")
+    _rowmajor(a_pad, BF16, "a_pad")
+    _rowmajor(bt_pad, BF16, "bt_pad")
+    M, N = dY.shape
+    K = X.shape[1]
+    if X.shape[0] != M or a_pad.shape[1] != K or bt_pad.shape[1] != N or a_pad.shape[0] < 16 \
+            or bt_pad.shape[0] < 16 or tuple(dA.shape) != (r, K) or tuple(dB.shape) != (N, r):
+        raise ValueError("lora_grad_1p: shape mismatch")
+    ws = splitk_workspace(torch.cuda.current_stream(dY.device))
+    call("lc_lora_grad_ws", stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
+         ptr(a_pad), a_pad.stride(0), ptr(bt_pad), bt_pad.stride(0), float(scaling), ptr(dA),
+         ptr(dB), ptr(ws), ws.numel())
+
+
 def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=None):
     M, D = z.shape
     call("lc_adapter_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),

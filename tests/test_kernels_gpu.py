@@ -36,7 +36,7 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 11])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 9, 10, 11])
 def test_gemm_nt_every_tile_exact(ops, dev, tile):
     """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
     the fused QuickGELU-derivative epilogue against torch at bf16 tolerance."""
@@ -111,7 +111,7 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
                                    (296 * 256 - 100, 256, 2048)])
-@pytest.mark.parametrize("tile", [0, 8])
+@pytest.mark.parametrize("tile", [0, 8, 9, 10])
 def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
     from lcclip import _lib
     lib = _lib.load()
@@ -586,3 +586,37 @@ def test_cast_weights_batch(ops, dev):
         assert torch.equal(out, W.to(BF))
         if outT is not None:
             assert torch.equal(outT, W.t().to(BF))
+
+
+@pytest.mark.parametrize("M,K,N", [(50432, 768, 2304), (3000 + 17, 768, 768), (770, 512, 1536),
+                                   (31, 512, 512), (1, 768, 768)])
+def test_lora_grad_one_pass(ops, dev, M, K, N):
+    """The one-pass LoRA gradient kernel (lc_lora_grad_ws) vs torch fp32 on the same bf16
+    operands: dB += s dY^T (X A^T), dA += s (dY B)^T X, r = 4, accumulated into nonzero
+    buffers; ragged M (row blocks of 32 with clamped tail rows), a single row, both sites'
+    shapes of the image and text towers. XA and dYB are rounded to bf16 inside the kernel (the
+    MFMA operand), as in the four-GEMM form: 4e-3 relative."""
+    torch.manual_seed(M + N)
+    r, s = 4, 0.25
+    X = torch.randn(M, K, device=dev).to(BF)
+    dY = (torch.randn(M, N, device=dev) * 0.1).to(BF)
+    A = torch.randn(r, K, device=dev) * K ** -0.5
+    B = torch.randn(N, r, device=dev) * 0.3
+    a_pad = torch.zeros(64, K, device=dev, dtype=BF)
+    a_pad[:r] = A.to(BF)
+    bt_pad = torch.zeros(64, N, device=dev, dtype=BF)
+    bt_pad[:r] = B.t().to(BF)
+    dA0 = torch.randn(r, K, device=dev)
+    dB0 = torch.randn(N, r, device=dev)
+    dA, dB = dA0.clone(), dB0.clone()
+    ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, s, dA, dB)
+    xa = (X.float() @ a_pad[:r].float().t()).to(BF).float()
+    dyb = (dY.float() @ bt_pad[:r].float().t()).to(BF).float()
+    ref_b = s * dY.float().t() @ xa
+    ref_a = s * dyb.t() @ X.float()
+    assert rel(dB - dB0, ref_b) < 4e-3
+    assert rel(dA - dA0, ref_a) < 4e-3
+    # deterministic: the same call twice gives the same bits
+    dA2, dB2 = dA0.clone(), dB0.clone()
+    ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, s, dA2, dB2)
+    assert torch.equal(dA, dA2) and torch.equal(dB, dB2)

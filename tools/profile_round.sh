@@ -20,7 +20,7 @@ run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -
 run fetch 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $P/fetch -o p -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline
 run write 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $P/write -o p -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline
 python tools/pmc_traffic.py $P/fetch $P/write gpurun_out/${TAG}_gemm_traffic.json > gpurun_out/${TAG}_pmc.log 2>&1
-python tools/prof_summary.py $P/trace/run_kernel_stats.csv 9 40 > gpurun_out/${TAG}_kernel_summary.txt 2>&1
-python tools/trace_by_shape.py $P/trace/run_kernel_trace.csv 9 40 > gpurun_out/${TAG}_by_shape.txt 2>&1
+python tools/prof_summary.py $P/trace/run_kernel_stats.csv 8 40 > gpurun_out/${TAG}_kernel_summary.txt 2>&1
+python tools/trace_by_shape.py $P/trace/run_kernel_trace.csv 8 40 > gpurun_out/${TAG}_by_shape.txt 2>&1
 cp $P/trace/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
 echo done
