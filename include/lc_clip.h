@@ -264,6 +264,19 @@ int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, co
                    unsigned long long seed, const unsigned long long* seed_dev,
                    const float* resid, float* xout, long ldx, void* h);
 
+/* lc_adapter_fwd followed by the LayerNorm of its output, in one launch: xout and h as
+ * lc_adapter_fwd, then y = bf16(LayerNorm(xout) * gamma + beta) (fp32 statistics, eps 1e-5)
+ * with mean / rstd [M] saved — the ln_2 of the same block or the ln_1 of the next
+ * (model.py:194-200). z, resid and xout cross HBM once (separately: two GEMM launches and a
+ * LayerNorm launch re-reading xout). D in {512, 768}. Replaces: Adapter.forward
+ * (adapter.py:53-72) + the residual (model.py:440-441) + the next ln_x (model.py:194-200). */
+int lc_adapter_ln_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
+                      const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                      unsigned long long seed, const unsigned long long* seed_dev,
+                      const float* resid, float* xout, long ldx, void* hout,
+                      const float* gamma, const float* beta, void* y, long ldy, float* mean,
+                      float* rstd);
+
 /* Row-local adapter backward: dpre (bf16 [M,64]) and dz = gout + dpre Wd (bf16; dz = NULL
  * computes dpre only).
  * WuT = Wu^T [64,D], WdT = Wd^T [D,64] (bf16). Weight/bias gradients: lc_gemm_tn.

@@ -91,17 +91,6 @@ LC_DEV bf16x8 read_frag(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + swz(row, chunk) * 16);
 }
 
-// s_waitcnt lgkmcnt(n) for an n known after unrolling (0..15)
-LC_DEV void lgkm_wait_n(int n) {
-  switch (n) {
-#define LC_LGKM(k) case k: asm volatile("s_waitcnt lgkmcnt(" #k ")" ::: "memory"); break;
-    LC_LGKM(0) LC_LGKM(1) LC_LGKM(2) LC_LGKM(3) LC_LGKM(4) LC_LGKM(5) LC_LGKM(6) LC_LGKM(7)
-    LC_LGKM(8) LC_LGKM(9) LC_LGKM(10) LC_LGKM(11) LC_LGKM(12) LC_LGKM(13) LC_LGKM(14)
-    default: asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory"); break;
-#undef LC_LGKM
-  }
-}
-
 template <int N>
 LC_DEV void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -1183,225 +1172,6 @@ gemm_w4_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Two-workgroups-per-CU GEMM (256 x 128 tile, 256 threads = 4 waves: one wave per SIMD per
-// workgroup, each wave a 128 x 64 output = 8 x 4 subtiles, 128 accumulator registers). Two
-// resident workgroups per CU (72 KiB of LDS and <= 256 VGPRs each) put two independent waves on
-// every SIMD: while one workgroup runs its epilogue (LDS-staged stores of the finished tile) or
-// its ring prologue, the other one's MFMAs keep the matrix pipe busy — the 256 x 256 kernels run
-// one workgroup per CU and leave the pipe idle for the whole epilogue.
-// K is consumed in 32-deep steps through a 3-slot LDS ring (slot = A [256][32] + B [128][32]
-// bf16 in 64-B rows = 24 KiB, swizzle chunk ^ (((row >> 3) & 1) << 1), the ping-pong kernel's
-// layout); the DMA of step s+2 is issued at the start of step s, so every step has two steps of
-// MFMA time (its own wave's and the co-resident workgroup's) to land.
-// Hazards: RAW — each wave retires its own DMA of step s+1 (counted vmcnt) before the barrier
-// that ends step s; step s+1's fragments are read after it. WAR — slot (s+2)%3 == (s-1)%3 was
-// last read by step s-1's fragment reads, consumed by its MFMAs before the barrier that ends
-// step s-1; the DMA of step s+2 is issued after that barrier.
-template <int EPI, bool PF = false>
-__global__ void __launch_bounds__(256, 2)
-gemm2w_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
-              const bf16_t* __restrict__ B, long ldb, const float* __restrict__ bias,
-              float alpha, void* __restrict__ out0, long ldo0, void* __restrict__ out1,
-              long ldo1, const void* __restrict__ aux, long ldaux, EpiParams ep, SplitK sk) {
-  constexpr int BM = 256, BN = 128, WM = 2, WN = 2;
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 8 x 4 subtiles per wave
-  constexpr int SLOT = (BM + BN) * 64;                 // 24 KiB
-  constexpr int NSLOT = 3;
-  constexpr int PA = BM / 16 / 4, PB = BN / 16 / 4;     // 1-KiB DMA pieces per wave per step (4 + 2)
-  constexpr int PIECES = PA + PB;
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int tiles_n = N / BN;
-  int bid = blockIdx.x;
-  int split = -1;
-  int sb = 0, se = K / 32;  // k-steps [sb, se) of this workgroup
-  if (bid < sk.dp_tiles) {
-    const int nwg = sk.dp_tiles;
-    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
-  } else {
-    const int s_id = bid - sk.dp_tiles;
-    split = s_id % sk.splits;
-    bid = sk.dp_tiles + s_id / sk.splits;
-    const int ns_all = K / 32;
-    sb = split * ns_all / sk.splits;
-    se = (split + 1) * ns_all / sk.splits;
-  }
-  int tm, tn;
-  tile_coords(bid, (M + BM - 1) / BM, tiles_n, ep.group_m, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int ns = se - sb;
-
-  // DMA pieces of this wave: A blocks wave, wave+4, .. (16 rows x 64 B each), B blocks likewise;
-  // source element offsets computed once (a step adds 32 k), LDS destinations are immediates
-  const int pr = lane >> 2;
-  int offa[PA], offb[PB];
-#pragma unroll
-  for (int p = 0; p < PA; ++p) {
-    const int r = (p * 4 + wave) * 16 + pr;
-    int gr = m0 + r;
-    gr = gr < M ? gr : M - 1;  // tail rows computed, never stored
-    offa[p] = gr * (int)lda + sb * 32 + swz64(r, lane & 3) * 8;
-  }
-#pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    const int r = (p * 4 + wave) * 16 + pr;
-    int gr = n0 + r;
-    gr = gr < N ? gr : N - 1;
-    offb[p] = gr * (int)ldb + sb * 32 + swz64(r, lane & 3) * 8;
-  }
-  auto dma_step = [&](int s, char* sl) {
-#pragma unroll
-    for (int p = 0; p < PA; ++p) glds16(A + offa[p] + s * 32, sl + (p * 4 + wave) * 1024);
-#pragma unroll
-    for (int p = 0; p < PB; ++p) glds16(B + offb[p] + s * 32, sl + BM * 64 + (p * 4 + wave) * 1024);
-  };
-  // fragment read offsets: the swizzle term depends on the lane only (subtiles start at
-  // multiples of 16 rows), so subtile i is the base + i KiB
-  const int g = lane >> 4, t = lane & 15;
-  const uint32_t fa0 = (wm * 128 + t) * 64 + swz64(t, g) * 16;
-  const uint32_t fb0 = BM * 64 + (wn * 64 + t) * 64 + swz64(t, g) * 16;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  dma_step(0, smem);
-  if (ns > 1) {
-    dma_step(1, smem + SLOT);
-    wait_vmcnt<PIECES>();
-  } else {
-    wait_vmcnt<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  int cur = 0;
-  if constexpr (PF) {
-    // PF: the fragments of step s+1 are read during step s's MFMAs (two register sets), so a
-    // wave never waits on LDS latency; the DMA of step s+2 (issued at step s) then has one step
-    // to land (waited at the top of step s+1, before the barrier that publishes its slot).
-    auto read_all = [&](uint32_t sl, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[j]) : "v"(sl + fb0), "n"(j * 1024));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[i]) : "v"(sl + fa0), "n"(i * 1024));
-    };
-    bf16x8 fa0_[TM], fb0_[TN], fa1_[TM], fb1_[TN];
-    read_all(lds0, fa0_, fb0_);
-    auto step = [&](int s, const bf16x8 (&fa)[TM], const bf16x8 (&fb)[TN], bf16x8 (&na)[TM],
-                    bf16x8 (&nb)[TN]) {
-      if (s + 1 < ns) wait_vmcnt<0>();  // own DMA of step s+1 (the only one in flight)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments of step s in registers
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      const int nx = cur == 0 ? 2 : cur - 1;  // slot of step s + 2 == slot of step s - 1
-      if (s + 2 < ns) dma_step(s + 2, smem + nx * SLOT);
-      const int c1 = cur == 2 ? 0 : cur + 1;
-      const uint32_t nsl = lds0 + c1 * SLOT;
-      const bool rd = s + 1 < ns;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-        if (rd) {
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(na[i]) : "v"(nsl + fa0), "n"(i * 1024));
-          if (i < TN)
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(nb[i]) : "v"(nsl + fb0), "n"(i * 1024));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      cur = c1;
-    };
-    int s = 0;
-    for (; s + 1 < ns; s += 2) {
-      step(s, fa0_, fb0_, fa1_, fb1_);
-      step(s + 1, fa1_, fb1_, fa0_, fb0_);
-    }
-    if (s < ns) step(s, fa0_, fb0_, fa1_, fb1_);
-    __builtin_amdgcn_s_barrier();  // every wave done with the ring
-  } else
-  for (int s = 0; s < ns; ++s) {
-    const int nx = cur == 0 ? 2 : cur - 1;  // slot of step s + 2 == slot of step s - 1
-    if (s + 2 < ns) dma_step(s + 2, smem + nx * SLOT);
-    // all 12 fragment reads up front (inline asm: hipcc would issue them two at a time, each
-    // pair behind an lgkmcnt(0)), then row group i's MFMAs behind a counted wait for its reads
-    const uint32_t sl = lds0 + cur * SLOT;
-    bf16x8 fa[TM], fb[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fb[j]) : "v"(sl + fb0), "n"(j * 1024));
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[i]) : "v"(sl + fa0), "n"(i * 1024));
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      lgkm_wait_n(TM - 1 - i);  // B's reads and A's 0..i landed
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // step s+1 landed (this wave's pieces); step s+2 may stay in flight
-    if (s + 2 < ns) wait_vmcnt<PIECES>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-  if (split >= 0) {
-    const int tail = bid - sk.dp_tiles;
-    constexpr int SLAB = BM * BN;
-    float* mine = sk.slabs + ((long)tail * sk.splits + split) * SLAB;
-    const int lane_off = (wave * TM * TN * 64 + lane) * 4;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        *reinterpret_cast<f32x4*>(mine + lane_off + (i * TN + j) * 256) = acc[i][j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int ticket = __hip_atomic_fetch_add(sk.tickets + tail, 1, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      const int last = ticket == sk.splits - 1;
-      if (last) {
-        __hip_atomic_store(sk.tickets + tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    const int last = flag[0];
-    __syncthreads();
-    if (!last) return;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < sk.splits; ++sp) {
-      const float* other = sk.slabs + ((long)tail * sk.splits + sp) * SLAB;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] += *reinterpret_cast<const f32x4*>(other + lane_off + (i * TN + j) * 256);
-    }
-  }
-  store_tile<BM, BN, WM, WN, EPI>(acc, smem, NSLOT * SLOT, m0, n0, M, bias, alpha, out0, ldo0,
-                                  out1, ldo1, aux, ldaux, ep);
-}
-
-// ---------------------------------------------------------------------------------------------
 // TN split-K GEMM: C[N1,N2] += alpha * sum_m A[m][n1] * B[m][n2].
 // 64x64 output tile per workgroup, 4 waves (2x2, 32x32 each), K-step = 64 rows of M staged
 // row-major in LDS and read TRANSPOSED with ds_read_b64_tr_b16 (4 rows x 16 cols per 16-lane
@@ -1944,36 +1714,6 @@ int launch_pp(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
   LC_LAUNCH_RET();
 }
 
-// Two-workgroups-per-CU 256x128 GEMM (gemm2w_kernel).
-template <bool PF>
-int launch_2w(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
-              const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
-              void* o1, long l1, const void* aux, long la, const EpiParams& ep_in, void* ws,
-              long ws_bytes) {
-  EpiParams ep = ep_in;
-  ep.group_m = group_m(N);
-  const int tiles = ((M + 255) / 256) * (N / 128);
-  const SplitK sk = plan_split(tiles, K / 32, 8, ws, ws_bytes, 2, 256 * 128);
-  dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(256);
-#define LC_2W_CASE(E)                                                                          \
-  case E:                                                                                      \
-    hipLaunchKernelGGL((gemm2w_kernel<E, PF>), grid, block, 0, st, M, N, K, A, lda, B, ldb, bias, \
-                       alpha, o0, l0, o1, l1, aux, la, ep, sk);                                \
-    break;
-  switch (epi) {
-    LC_2W_CASE(EPI_BF16)
-    LC_2W_CASE(EPI_F32)
-    LC_2W_CASE(EPI_RESID)
-    LC_2W_CASE(EPI_GELU)
-    LC_2W_CASE(EPI_GELU_D)
-    LC_2W_CASE(EPI_MUL)
-    default:
-      return LC_EINVAL;
-  }
-#undef LC_2W_CASE
-  LC_LAUNCH_RET();
-}
-
 // Phase-interleaved 256x256 GEMM (gemm8_kernel). bf16: A, B bf16 with lda/ldb in elements;
 // fp8: A, B e4m3 with lda/ldb in bytes and their E8M0 scales in sc.
 template <bool FP8>
@@ -2070,11 +1810,8 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     // 37 -> 35 us)
     if (K <= 64) tile = 11;
   }
-  if ((tile == 9 || tile == 10) && (epi > EPI_MUL || epi == EPI_GELU_BWD || epi == EPI_BF16_F32 ||
-                    (long)M * (lda > ldb ? lda : ldb) >= (1L << 31)))
-    tile = 8;
   if (((tile == 3 || tile == 5 || tile == 6 || tile == 7 || tile == 8) && N % 256) ||
-      ((tile == 1 || tile == 2 || tile == 9 || tile == 10) && N % 128))
+      ((tile == 1 || tile == 2) && N % 128))
     tile = 4;
   switch (tile) {
     case 1:
@@ -2100,12 +1837,6 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
                          aux, ldaux, ep, ws, ws_bytes);
       return launch_g8<false>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1,
                               ldo1, aux, ldaux, ep, ws, ws_bytes, Fp8Scales{});
-    case 10:  // the same with fragment prefetch
-      return launch_2w<true>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1,
-                             ldo1, aux, ldaux, ep, ws, ws_bytes);
-    case 9:  // 256x128, two workgroups per CU
-      return launch_2w<false>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
-                       aux, ldaux, ep, ws, ws_bytes);
     case 11:  // 128x64, one LDS stage
       return launch_nt<128, 64, 4, 1, 1>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0,
                                          ldo0, out1, ldo1, aux, ldaux, ep);

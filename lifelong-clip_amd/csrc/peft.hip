@@ -544,7 +544,7 @@ struct LoraGeom {
   static constexpr int BYTES = DYBT_OFF + 1024;
   static constexpr int XKS = KT / 8;              // XA k-steps per wave
   static constexpr int DAT = KT * 2 / 8;          // dA 16-column tiles per wave
-  static constexpr int SLOT_FLOATS = NC * 128 * 16 + 16 * K;  // dB [N][16] + dA [16][K]
+  // walker slot: dB [N][r] then dA [r][K] (r <= 16, only the real rank is stored)
 };
 
 LC_DEV void vm_wait_n(int n) {
@@ -562,7 +562,7 @@ __global__ void __launch_bounds__(512, 1)
 lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* __restrict__ dY,
                    long ldy, const bf16_t* __restrict__ apad, long lda,
                    const bf16_t* __restrict__ btpad, long ldbt, float* __restrict__ part,
-                   int walkers) {
+                   int walkers, int r) {
   using G = LoraGeom<KT, NC>;
   constexpr int K = G::K, XROW = G::XROW;
   __shared__ __attribute__((aligned(16))) char smem[G::BYTES];
@@ -717,48 +717,290 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
     for (int j = 0; j < G::DAT; ++j)
       accA[j] = mfma16(dyf, tr_frag<XROW>(ximg, 8 * g + (t >> 2), (wave * G::DAT + j) * 16 + (t & 3) * 4), accA[j]);
   }
-  // walker partial: dB [N][16] (lane: rows n = c*128 + wave*16 + 4g + rr, col r = t), dA [16][K]
-  // (lane: rows r = 4g + rr, col k = (wave*DAT + j)*16 + t)
-  float* slot_p = part + (long)cidx * G::SLOT_FLOATS;
+  // walker partial: dB [N][r] (lane: rows n = c*128 + wave*16 + 4g + rr, column t < r), dA [r][K]
+  // (lane: rows 4g + rr < r, column k = (wave*DAT + j)*16 + t)
+  constexpr int N = NC * 128;
+  float* slot_p = part + (long)cidx * ((long)N * r + (long)r * K);
+  if (t < r) {
 #pragma unroll
-  for (int c = 0; c < NC; ++c)
+    for (int c = 0; c < NC; ++c)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-      slot_p[(c * 128 + wave * 16 + 4 * g + rr) * 16 + t] = accB[c][rr];
+      for (int rr = 0; rr < 4; ++rr)
+        slot_p[(c * 128 + wave * 16 + 4 * g + rr) * r + t] = accB[c][rr];
+  }
 #pragma unroll
   for (int j = 0; j < G::DAT; ++j)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr)
-      slot_p[NC * 128 * 16 + (4 * g + rr) * K + (wave * G::DAT + j) * 16 + t] = accA[j][rr];
+      if (4 * g + rr < r)
+        slot_p[(long)N * r + (4 * g + rr) * K + (wave * G::DAT + j) * 16 + t] = accA[j][rr];
 }
 
-// dB[n][j] += s * sum_w part_w dB[n][j],  dA[j][k] += s * sum_w part_w dA[j][k]  (j < r)
+// dB[n][j] += s * sum_w part_w dB[n][j],  dA[j][k] += s * sum_w part_w dA[j][k]  (j < r): the
+// walker slots are [N r | r K] floats (the output's own layout), so output e sums element e of
+// every slot. 8 threads per output each sum every 8th walker, then one of them adds the 8 in
+// order (deterministic); 32 outputs per 256-thread workgroup.
 __global__ void __launch_bounds__(256)
-lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats, int N, int K,
-                   int r, float s, float* __restrict__ dA, float* __restrict__ dB) {
-  const int nb = N * r, na = r * K;
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < nb + na; e += gridDim.x * 256) {
-    long off;
-    float* dst;
-    if (e < nb) {
-      const int n = e / r, j = e % r;
-      off = (long)n * 16 + j;
-      dst = dB + (long)n * r + j;
-    } else {
-      const int j = (e - nb) / K, k = (e - nb) % K;
-      off = (long)N * 16 + (long)j * K + k;
-      dst = dA + (long)j * K + k;
-    }
-    float v = 0.f;
-    int w = 0;
-    for (; w + 8 <= walkers; w += 8) {
+lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats, long nb,
+                   float s, float* __restrict__ dA, float* __restrict__ dB) {
+  __shared__ float red[8][33];
+  const int lo = threadIdx.x & 31, wg = threadIdx.x >> 5;
+  const long e = (long)blockIdx.x * 32 + lo;
+  float v = 0.f;
+  if (e < slot_floats) {
+    int w = wg;
+    for (; w + 56 < walkers; w += 64) {
       float q[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] = part[(long)(w + u) * slot_floats + off];
+      for (int u = 0; u < 8; ++u) q[u] = part[(long)(w + 8 * u) * slot_floats + e];
       v += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     }
-    for (; w < walkers; ++w) v += part[(long)w * slot_floats + off];
-    *dst += s * v;
+    for (; w < walkers; w += 8) v += part[(long)w * slot_floats + e];
+  }
+  red[wg][lo] = v;
+  __syncthreads();
+  if (wg == 0 && e < slot_floats) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += red[k][lo];
+    if (e < nb) dB[e] += s * tot;
+    else dA[e - nb] += s * tot;
+  }
+}
+
+
+// ------------------------------------------------- adapter forward + residual + LayerNorm, fused
+// One launch for the adapter sub-block of a block (adapter.py:53-72, model.py:440-441) and the
+// LayerNorm that reads its output next (ln_2 of the same block, or ln_1 of the next one,
+// model.py:194-200):
+//   h     = drop(relu(z Wd^T + bd))                (saved, bf16 [M, 64])
+//   x_out = resid + z + scale * (h Wu^T + bu)      (f32, the residual stream)
+//   y     = LN(x_out) * gamma + beta               (bf16, the next GEMM's A operand; mean, rstd saved)
+// Separately these are two skinny GEMM launches and a LayerNorm launch that re-reads x_out
+// (and z twice); here z, resid and x_out each cross HBM once. 16-row blocks; one persistent
+// 8-wave workgroup per CU; z of the next block comes by LDS-DMA and resid by (inline-asm) loads
+// while the current block computes. Both weights live in registers as MFMA fragments: the down
+// projection splits K = D over the waves (partials summed through LDS), the up projection gives
+// each wave D/8 output columns of all 16 rows. The row statistics of the LayerNorm (two-pass:
+// mean, then the mean of squared deviations, as ln_fwd_kernel) are summed over the waves in LDS.
+// The dropout mask is drop_mul(seed, row, j) — the EPI_AD_DOWN epilogue's — so the forward is
+// the separate path's, and the backward regenerates the same mask.
+template <int D>
+struct AdLnLay {
+  static constexpr int ZROW = D * 2;                 // z image row bytes
+  static constexpr int ZIMG = 16 * ZROW;             // one 16-row z block
+  static constexpr int ZP = ZIMG / 1024 / 8;         // z DMA pieces per wave
+  static constexpr int Z_OFF = 0;                    // two z buffers
+  static constexpr int RED_OFF = 2 * ZIMG;           // [8][16][64] f32 down partials
+  static constexpr int H_OFF = RED_OFF + 8 * 16 * 64 * 4;   // h block bf16 [16][64]
+  static constexpr int ST_OFF = H_OFF + 16 * 64 * 2;        // [2][8][16] f32 row sums
+  static constexpr int PRM_OFF = ST_OFF + 2 * 8 * 16 * 4;   // bu, gamma, beta f32 [3][D]
+  static constexpr int BYTES = PRM_OFF + 3 * D * 4;
+  static constexpr int KS = D / 32 / 8;              // down-projection k-steps per wave
+  static constexpr int NU = D / 8 / 16;              // up-projection 16-column tiles per wave
+};
+
+template <int D>
+__global__ void __launch_bounds__(512, 1)
+adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_t* __restrict__ Wd,
+                      const float* __restrict__ bd, const bf16_t* __restrict__ Wu,
+                      const float* __restrict__ bu, float scale, float keep, uint64_t seed,
+                      const unsigned long long* __restrict__ seed_dev,
+                      const float* __restrict__ resid, float* __restrict__ xout, long ldx,
+                      bf16_t* __restrict__ hout, const float* __restrict__ gamma,
+                      const float* __restrict__ beta, bf16_t* __restrict__ y, long ldy,
+                      float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  using L = AdLnLay<D>;
+  constexpr int KS = L::KS, NU = L::NU;
+  __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, t = lane & 15;
+  const int nblk = (M + 15) / 16;
+  if ((int)blockIdx.x >= nblk) return;
+  if (seed_dev) seed += *seed_dev * 0xD1B54A32D192ED03ull;
+  float* red = reinterpret_cast<float*>(smem + L::RED_OFF);
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem + L::H_OFF);
+  float* st = reinterpret_cast<float*>(smem + L::ST_OFF);
+  float* prm = reinterpret_cast<float*>(smem + L::PRM_OFF);
+  for (int e = tid; e < D; e += 512) {
+    prm[e] = bu[e];
+    prm[D + e] = gamma[e];
+    prm[2 * D + e] = beta[e];
+  }
+  // weights as fragments (inline-asm loads: invisible to hipcc's vmcnt bookkeeping, retired
+  // by the explicit wait below before any LDS-DMA is in flight)
+  //   down: B[k][j] = Wd[j][k], lane (t, g): Wd row (16 n + t), k = (wave KS + ks) 32 + 8g ..
+  //   up:   B[k][j] = Wu[j][k], lane (t, g): Wu row (wave D/8 + 16 u + t), k = 32 ks + 8g ..
+  bf16x8 wdf[KS][4], wuf[NU][2];
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=v"(wdf[k][n])
+                   : "v"(Wd + (long)(16 * n + t) * D + (wave * KS + k) * 32 + 8 * g));
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=v"(wuf[u][k])
+                   : "v"(Wu + (long)(wave * (D / 8) + 16 * u + t) * 64 + 32 * k + 8 * g));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // z block b -> buffer buf: 1-KiB pieces, lane -> (row, 16-B position) inverting the 32-B
+  // unit swizzle (swz_w: conflict-free row reads and 8-B epilogue reads)
+  auto dma_z = [&](int b, int buf) {
+    char* dst = smem + L::Z_OFF + buf * L::ZIMG;
+    const int r0 = b * 16;
+#pragma unroll
+    for (int pp = 0; pp < L::ZP; ++pp) {
+      const int piece = wave * L::ZP + pp;
+      const int idx = piece * 64 + lane;
+      const int row = idx / (L::ZROW / 16), pc = idx % (L::ZROW / 16);
+      const int c = (((pc >> 1) ^ swz_w(row)) << 1) | (pc & 1);
+      const int m = min(r0 + row, M - 1);
+      glds16(z + (long)m * ldz + c * 8, dst + piece * 1024);
+    }
+  };
+  auto zaddr = [&](const char* img, int row, int byte) {  // byte offset within the row
+    const int u = (byte >> 5) ^ swz_w(row);
+    return img + row * L::ZROW + u * 32 + (byte & 31);
+  };
+  // resid of block b for this lane's outputs: row t, columns wave D/8 + 16 u + 4 g .. +3
+  auto load_x = [&](int b, f32x4 (&xr)[NU]) {
+    const int m = min(b * 16 + t, M - 1);
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      asm volatile("global_load_dwordx4 %0, %1, off"
+                   : "=v"(xr[u])
+                   : "v"(resid + (long)m * ldx + wave * (D / 8) + 16 * u + 4 * g));
+  };
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4 xa[NU], xb[NU];
+  int b = blockIdx.x;
+  dma_z(b, 0);
+  load_x(b, xa);
+  // buf: this walker's iteration parity (the z double buffer; blocks b and b + gridDim.x can
+  // have the same index parity)
+  auto body = [&](int b, int buf, f32x4 (&xr)[NU], f32x4 (&xn)[NU]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // z_b, resid_b, and the last block's stores
+    __syncthreads();  // also publishes prm on the first block
+    const int bn = b + gridDim.x;
+    if (bn < nblk) {
+      dma_z(bn, buf ^ 1);  // the other buffer: read by the previous block only
+      load_x(bn, xn);
+    }
+    const char* zi = smem + L::Z_OFF + buf * L::ZIMG;
+    const int r0 = b * 16;
+    // ---- down projection: partial over this wave's KS k-steps, all 64 bottleneck columns
+    {
+      f32x4 pd[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) pd[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int byte = ((wave * KS + k) * 32 + 8 * g) * 2;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(zaddr(zi, t, byte));
+#pragma unroll
+        for (int n = 0; n < 4; ++n) pd[n] = mfma16(a, wdf[k][n], pd[n]);
+      }
+      // lane holds P[m = 4g + rr][j = 16n + t]
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) red[(wave * 16 + 4 * g + rr) * 64 + 16 * n + t] = pd[n][rr];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // 1024 outputs, 2 per thread
+      const int e = tid + 512 * q, m = e >> 6, j = e & 63;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += red[(w * 16 + m) * 64 + j];
+      v = fmaxf(v + bd[j], 0.f) * drop_mul(seed, (long)(r0 + m), j, keep);
+      const bf16_t hb = f2bf(v);
+      hs[m * 64 + j] = hb;
+      if (r0 + m < M) hout[(long)(r0 + m) * 64 + j] = hb;
+    }
+    lds_barrier();
+    // ---- up projection: rows t of the block (A = h), this wave's D/8 columns (B = Wu)
+    const bf16x8 ha0 = *reinterpret_cast<const bf16x8*>(hs + t * 64 + 8 * g);
+    const bf16x8 ha1 = *reinterpret_cast<const bf16x8*>(hs + t * 64 + 32 + 8 * g);
+    f32x4 xo[NU];
+    float s1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      f32x4 acc = mfma16(wuf[u][0], ha0, f32x4{0.f, 0.f, 0.f, 0.f});
+      acc = mfma16(wuf[u][1], ha1, acc);
+      // lane holds U[m = t][n = col + rr], col = wave D/8 + 16u + 4g (the swapped layout)
+      const int col = wave * (D / 8) + 16 * u + 4 * g;
+      const uint2 zz = *reinterpret_cast<const uint2*>(zaddr(zi, t, col * 2));
+      const float zf[4] = {bf2f(zz.x & 0xffff), bf2f(zz.x >> 16), bf2f(zz.y & 0xffff), bf2f(zz.y >> 16)};
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const float v = acc[rr] + prm[col + rr];
+        xo[u][rr] = xr[u][rr] + zf[rr] + scale * v;
+        s1 += xo[u][rr];
+      }
+    }
+    const bool live = r0 + t < M;
+    if (live) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        *reinterpret_cast<f32x4*>(xout + (long)(r0 + t) * ldx + wave * (D / 8) + 16 * u + 4 * g) = xo[u];
+    }
+    // ---- LayerNorm of the 16 rows: sums over the 4 lanes of a row, then over the waves
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    if (g == 0) st[wave * 16 + t] = s1;
+    lds_barrier();
+    float mean = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) mean += st[w * 16 + t];
+    mean *= 1.0f / D;
+    float s2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        xo[u][rr] -= mean;
+        s2 += xo[u][rr] * xo[u][rr];
+      }
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    if (g == 0) st[128 + wave * 16 + t] = s2;
+    lds_barrier();
+    float var = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) var += st[128 + w * 16 + t];
+    const float rstd = rsqrtf(var * (1.0f / D) + 1e-5f);
+    if (live) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int col = wave * (D / 8) + 16 * u + 4 * g;
+        float o[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) o[rr] = xo[u][rr] * rstd * prm[D + col + rr] + prm[2 * D + col + rr];
+        *reinterpret_cast<uint2*>(y + (long)(r0 + t) * ldy + col) =
+            uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+      }
+      if (wave == 0 && g == 0) {
+        mean_out[r0 + t] = mean;
+        rstd_out[r0 + t] = rstd;
+      }
+    }
+  };
+#pragma unroll 1
+  for (; b < nblk; b += 2 * gridDim.x) {
+    body(b, 0, xa, xb);
+    if (b + (int)gridDim.x < nblk) body(b + gridDim.x, 1, xb, xa);
   }
 }
 
@@ -833,23 +1075,22 @@ int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, 
       cus = 256;
     walkers = nblk < cus ? nblk : cus;
   }
-  const long slot = (long)N * 16 + 16L * K;
+  const long slot = (long)N * r + (long)r * K;
   LC_CHECK_ARG(ws_bytes >= LC_SPLITK_TICKET_BYTES + (long)walkers * slot * 4);
   float* part = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
 #define LC_LG(KT, NC)                                                                           \
   if (K == KT * 32 && N == NC * 128) {                                                         \
     hipLaunchKernelGGL((lora_grad1p_kernel<KT, NC>), dim3(walkers), dim3(512), 0, st, M,        \
                        (const bf16_t*)X, ldx, (const bf16_t*)dY, ldy, (const bf16_t*)apad, lda, \
-                       (const bf16_t*)btpad, ldbt, part, walkers);                             \
+                       (const bf16_t*)btpad, ldbt, part, walkers, r);                          \
   } else
   LC_LG(24, 18) LC_LG(24, 6) LC_LG(16, 12) LC_LG(16, 4)
   { return LC_EINVAL; }
 #undef LC_LG
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return LC_ELAUNCH;
-  const int tot = N * r + r * K;
-  hipLaunchKernelGGL(lora_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, part, walkers,
-                     slot, N, K, r, scaling, dA, dB);
+  hipLaunchKernelGGL(lora_reduce_kernel, dim3((unsigned)((slot + 31) / 32)), dim3(256), 0, st,
+                     part, walkers, slot, (long)N * r, scaling, dA, dB);
   LC_LAUNCH_RET();
 }
 
@@ -869,6 +1110,32 @@ int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const 
   if (rc) return rc;
   return lc_gemm_nt_ex(st, 9 /*EPI_AD_UP*/, M, D, AD_H, hout, AD_H, Wu, AD_H, bu, 1.0f, xout, ldx,
                        nullptr, 0, resid, ldx, ep);
+}
+
+int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
+                      const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                      unsigned long long seed, const unsigned long long* seed_dev,
+                      const float* resid, float* xout, long ldx, void* hout,
+                      const float* gamma, const float* beta, void* y, long ldy, float* mean,
+                      float* rstd) {
+  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldz % 8 == 0 && ldx % 4 == 0 && ldy % 4 == 0);
+  LC_CHECK_ARG(ldz >= D && ldx >= D && ldy >= D && keep > 0.f && keep <= 1.f);
+  LC_CHECK_ARG(z && Wd && bd && Wu && bu && resid && xout && hout && gamma && beta && y && mean && rstd);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  const int nblk = (M + 15) / 16;
+  const int grid = nblk < cus ? nblk : cus;
+#define LC_ALN(DD)                                                                               \
+  hipLaunchKernelGGL(adapter_ln_fwd_kernel<DD>, dim3(grid), dim3(512), 0, st, M,                 \
+                     (const bf16_t*)z, ldz, (const bf16_t*)Wd, bd, (const bf16_t*)Wu, bu, scale,  \
+                     keep, (uint64_t)seed, seed_dev, resid, xout, ldx, (bf16_t*)hout, gamma,     \
+                     beta, (bf16_t*)y, ldy, mean, rstd)
+  if (D == 768) LC_ALN(768);
+  else LC_ALN(512);
+#undef LC_ALN
+  LC_LAUNCH_RET();
 }
 
 //   dpre = (h > 0) ? scale * (gout Wu) / keep : 0    [M,64]  N = 64, K = D   (B = Wu^T)

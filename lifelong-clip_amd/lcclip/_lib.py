@@ -54,6 +54,8 @@ SIGNATURES = {
                         c_float, P, P, P, c_long],
     "lc_adapter_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong, P, P,
                        P, c_long, P],
+    "lc_adapter_ln_fwd": [P, c_int, c_int, P, c_long, P, P, P, P, c_float, c_float, c_ulonglong,
+                          P, P, P, c_long, P, P, P, P, c_long, P, P],
     "lc_adapter_bwd": [P, c_int, c_int, P, c_long, P, P, P, c_float, c_float, P, P, c_long],
     "lc_adapter_wgrad": [P, c_int, c_int, P, c_long, P, P, c_long, P, c_float, P, P, P, P],
     "lc_adapter_wgrad_ws": [P, c_int, c_int, P, c_long, P, P, c_long, P, c_float, P, P, P, P, P,

@@ -189,6 +189,9 @@ class BlockStack:
     # quant_fp8 pass (the same codes). LCCLIP_FP8_FUSE for A/Bs: 0 none, 1 the GEMM epilogues,
     # 2 + LayerNorm, 3 (default) + attention backward
     FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "3"))
+    # bf16 adapter towers: adapter + the following LayerNorm in one launch (LCCLIP_FUSE_LN=0: the
+    # separate adapter_fwd + layernorm_fwd launches, for A/Bs)
+    FUSE_LN = os.environ.get("LCCLIP_FUSE_LN", "1") != "0"
 
     def _fused_q8(self, level=1):
         return self.precision == "fp8" and self.FUSE_Q8 >= level
@@ -240,6 +243,11 @@ class BlockStack:
         tmp_g = _empty((Mmax, 4 * D), BF16, dev) if q_g is None else None
         tmp_pre = None if save else _empty((Mmax, 4 * D), BF16, dev)
         saved = [] if save else None
+        # bf16 adapter towers: each adapter runs fused with the LayerNorm that reads its output
+        # (ops.adapter_ln_fwd: ln_2 of the block, ln_1 of the next one); ln1_ready carries the
+        # statistics of an ln_1 the previous block already wrote into tmp_h
+        fuse_ln = (self.variant == "adapter" and q_h is None and D in (512, 768) and self.FUSE_LN)
+        ln1_ready = None
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
             if stop is not None and idx >= stop:
                 break
@@ -268,8 +276,12 @@ class BlockStack:
                                            mean1, rstd1, y=None if h1 is th else h1)
                 ops.gemm_nt_fp8(qa, st.q["wqkv"], EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
             else:
-                ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
+                if ln1_ready is not None:  # written by the previous block's fused adapter
+                    mean1, rstd1 = ln1_ready
+                else:
+                    ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
                 self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
+            ln1_ready = None
             O = _empty((Mx, D), BF16, dev)
             lse = _empty((n_seq * H, Lx), F32, dev)
             ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
@@ -281,13 +293,23 @@ class BlockStack:
                 z1 = _empty((Mx, D), BF16, dev)
                 ops.gemm_nt(O, st.wo, EPI_BF16, z1, bias=blk.attn.out_proj.bias)
                 hd1 = _empty((Mx, ad.down_size), BF16, dev)
-                ops.adapter_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale, keep,
-                                seed1, x, x_mid, hd1, seed_dev=self.seed_dev)
+                mean2 = _empty((Mx,), F32, dev)
+                rstd2 = _empty((Mx,), F32, dev)
+                if fuse_ln and q_g is None:
+                    ops.adapter_ln_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias,
+                                       ad.scale, keep, seed1, x, x_mid, hd1, blk.ln_2.weight,
+                                       blk.ln_2.bias, th, mean2, rstd2, seed_dev=self.seed_dev)
+                    ln2_done = True
+                else:
+                    ops.adapter_fwd(z1, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
+                                    keep, seed1, x, x_mid, hd1, seed_dev=self.seed_dev)
+                    ln2_done = False
                 s.update(z1=z1, hd1=hd1, keep=keep)
             else:
                 ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
-            mean2 = _empty((Mx,), F32, dev)
-            rstd2 = _empty((Mx,), F32, dev)
+                mean2 = _empty((Mx,), F32, dev)
+                rstd2 = _empty((Mx,), F32, dev)
+                ln2_done = False
             pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
             if q_g is not None:
@@ -303,7 +325,8 @@ class BlockStack:
                                        bias=blk.mlp.c_fc.bias, q_out=q_g.narrow(Mx))
                 wpr = lambda epi, out0, **kw: ops.gemm_nt_fp8(g_in, st.q["wpr"], epi, out0, **kw)  # noqa: E731
             else:
-                ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
+                if not ln2_done:
+                    ops.layernorm_fwd(x_mid, blk.ln_2.weight, blk.ln_2.bias, th, mean2, rstd2)
                 self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
                            bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
                 wpr = lambda epi, out0, **kw: self._gemm(st, "wpr", tmp_g[:Mx], epi, out0, **kw)  # noqa: E731
@@ -314,8 +337,21 @@ class BlockStack:
                 z2 = _empty((Mx, D), BF16, dev)
                 wpr(EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
                 hd2 = _empty((Mx, ad.down_size), BF16, dev)
-                ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
-                                s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
+                nxt = idx + 1
+                if (fuse_ln and nxt < len(self.blocks) and (stop is None or nxt < stop)
+                        and not P_of.get(nxt, 0) and not P and not (replace and nxt in replace)):
+                    # the next block's ln_1 into tmp_h (c_fc has consumed it by now: same stream)
+                    nb = self.blocks[nxt]
+                    m1 = _empty((Mx,), F32, dev)
+                    r1 = _empty((Mx,), F32, dev)
+                    ops.adapter_ln_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias,
+                                       ad.scale, s["keep"], seed2, x_mid, x_out, hd2,
+                                       nb.ln_1.weight, nb.ln_1.bias, th, m1, r1,
+                                       seed_dev=self.seed_dev)
+                    ln1_ready = (m1, r1)
+                else:
+                    ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
+                                    s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
                 wpr(EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)

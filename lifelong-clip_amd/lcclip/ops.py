@@ -320,6 +320,18 @@ def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=N
          ptr(resid), ptr(xout), xout.stride(0), ptr(h))
 
 
+def adapter_ln_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, gamma, beta, y, mean,
+                   rstd, seed_dev=None):
+    """adapter_fwd, then y = LayerNorm(xout) (bf16, statistics saved) in one launch."""
+    M, D = z.shape
+    if y.dtype != BF16 or tuple(y.shape) != (M, D) or y.stride(1) != 1:
+        raise ValueError("adapter_ln_fwd: y must be a bf16 [M, D] row-major view")
+    call("lc_adapter_ln_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
+         ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
+         ptr(resid), ptr(xout), xout.stride(0), ptr(h), ptr(gamma), ptr(beta), ptr(y),
+         y.stride(0), ptr(mean), ptr(rstd))
+
+
 def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
     M, D = gout.shape
     call("lc_adapter_bwd", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),

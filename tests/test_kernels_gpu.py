@@ -36,7 +36,7 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 11])
 def test_gemm_nt_every_tile_exact(ops, dev, tile):
     """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
     the fused QuickGELU-derivative epilogue against torch at bf16 tolerance."""
@@ -111,7 +111,7 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
                                    (296 * 256 - 100, 256, 2048)])
-@pytest.mark.parametrize("tile", [0, 8, 9, 10])
+@pytest.mark.parametrize("tile", [0, 8])
 def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
     from lcclip import _lib
     lib = _lib.load()
@@ -620,3 +620,36 @@ def test_lora_grad_one_pass(ops, dev, M, K, N):
     dA2, dB2 = dA0.clone(), dB0.clone()
     ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, s, dA2, dB2)
     assert torch.equal(dA, dA2) and torch.equal(dB, dB2)
+
+
+@pytest.mark.parametrize("M,D,keep", [(50432, 768, 1.0), (3000 + 5, 768, 0.9), (770, 512, 1.0),
+                                      (7, 512, 0.9)])
+def test_adapter_ln_fwd_matches_separate(ops, dev, M, D, keep):
+    """The fused adapter + LayerNorm forward (lc_adapter_ln_fwd) against the separate
+    lc_adapter_fwd + lc_layernorm_fwd launches on the same inputs: same dropout mask (same
+    seed), x_out / mean / rstd to f32 rounding, h and the LayerNorm output to bf16 rounding
+    (the down projection sums K over the waves in a different order, so a bf16 rounding of h
+    can flip); ragged M and a tail block of 7 rows."""
+    torch.manual_seed(M + D)
+    z = torch.randn(M, D, device=dev).to(BF)
+    Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
+    Wu = (torch.randn(D, 64, device=dev) * 0.125).to(BF)
+    bd = torch.randn(64, device=dev) * 0.1
+    bu = torch.randn(D, device=dev) * 0.1
+    x = torch.randn(M, D, device=dev) * 2
+    gam = torch.randn(D, device=dev)
+    bet = torch.randn(D, device=dev)
+    seed = 12345
+    xo1, h1 = torch.empty(M, D, device=dev), torch.empty(M, 64, device=dev, dtype=BF)
+    y1 = torch.empty(M, D, device=dev, dtype=BF)
+    m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    ops.adapter_fwd(z, Wd, bd, Wu, bu, 0.1, keep, seed, x, xo1, h1)
+    ops.layernorm_fwd(xo1, gam, bet, y1, m1, r1)
+    xo2, h2 = torch.empty_like(xo1), torch.empty_like(h1)
+    y2, m2, r2 = torch.empty_like(y1), torch.empty_like(m1), torch.empty_like(r1)
+    ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, keep, seed, x, xo2, h2, gam, bet, y2, m2, r2)
+    assert rel(h2, h1) < 4e-3
+    assert ((h1 == 0) != (h2 == 0)).float().mean().item() < 1e-3  # same relu / dropout zeros
+    assert rel(xo2, xo1) < 1e-5
+    assert rel(m2, m1) < 1e-5 and rel(r2, r1) < 1e-5
+    assert rel(y2, y1) < 4e-3
