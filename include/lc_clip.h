@@ -248,7 +248,7 @@ int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY,
  * workgroup per CU, partial sums in ws after its first LC_SPLITK_TICKET_BYTES (needs
  * walkers x (16 N + 16 K) x 4 B, walkers = min(CUs, ceil(M/32))) summed by a second launch in
  * walker order (deterministic). Shapes: (K, N) in {(768, 2304), (768, 768), (512, 1536),
- * (512, 512)} (ViT-B/16 image / text QKV and out-proj sites); r <= 16.
+ * (512, 512)} (ViT-B/16 image / text QKV and out-proj sites); r <= 4 (the reference's lora_r).
  * Replaces: autograd of the two F.linear LoRA products (lora.py:838-839, 1073-1074). */
 int lc_lora_grad_ws(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
                     const void* X, long ldx, const void* apad, long lda, const void* btpad,

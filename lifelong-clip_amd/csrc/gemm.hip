@@ -1421,21 +1421,29 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
     else if (STAGES > 3 && ahead == 2) wait_vmcnt<2 * LOADS>();
     else if (ahead >= 1) wait_vmcnt<LOADS>();
     else wait_vmcnt<0>();
-    __syncthreads();
+    lds_barrier();  // (__syncthreads would wait vmcnt(0): the whole ring)
     if (s + STAGES - 1 < nsteps) dma(s + STAGES - 1);
-    const char* sw = smem + (s % STAGES) * SLOT;
-    const char* ss = sw + Geo::WB;
+    const uint32_t sw = lds_addr(smem + (s % STAGES) * SLOT);
+    const uint32_t ss = sw + Geo::WB;
     const int valid = p.M - blk_row(s);  // rows of this block inside M (>= 64: all)
+    // both k-slices' fragments issued up front (asm reads: no compiler drain), one wait
+    bf16x8 fwk[2][TI], fsk[2][2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int row = ks * 32 + g * 8 + (t >> 2);
-      const int kb = ks * 32 + g * 8;
-      bf16x8 fw[TI], fs[2];
 #pragma unroll
       for (int i = 0; i < TI; ++i)
-        fw[i] = tr_frag<ROWB>(sw, row, wn * (PW / 4) + i * 16 + (t & 3) * 4);
+        fwk[ks][i] = tr_frag_asm<ROWB>(sw, row, wn * (PW / 4) + i * 16 + (t & 3) * 4);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fs[j] = tr_frag<128>(ss, row, wsv * 32 + j * 16 + (t & 3) * 4);
+      for (int j = 0; j < 2; ++j)
+        fsk[ks][j] = tr_frag_asm<128>(ss, row, wsv * 32 + j * 16 + (t & 3) * 4);
+    }
+    lds_wait0();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = ks * 32 + g * 8;
+      bf16x8* fw = fwk[ks];
+      bf16x8* fs = fsk[ks];
       bf16x8 ones;
 #pragma unroll
       for (int e = 0; e < 8; ++e) ones[e] = (kb + e < valid) ? one : (short)0;

@@ -190,6 +190,38 @@ LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// Reads of LDS-DMA images inside a streaming loop. hipcc cannot tell a ring slot that has landed
+// from the ones still in flight, so it puts s_waitcnt vmcnt(0) in front of a builtin LDS read of
+// a global_load_lds target and in front of __syncthreads() — draining the ring every step. The
+// forms below are inline asm: the caller owns the waits (lds_wait0 before the first use of a
+// result, counted vmcnt waits before the barrier that publishes a slot).
+LC_DEV uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+template <int ROWB>
+LC_DEV bf16x8 tr_frag_asm(uint32_t img, int row, int col) {
+  auto addr = [&](int r) {
+    const int byte = col * 2;
+    const int u = (byte >> 5) ^ (ROWB >= 256 ? swz_w(r) : swz_s(r));
+    return img + r * ROWB + u * 32 + (byte & 31);
+  };
+  bf16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(addr(row)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(addr(row + 4)));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// all issued LDS reads retired; nothing is scheduled across the wait
+LC_DEV void lds_wait0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+// workgroup barrier for LDS hand-offs while LDS-DMA stays in flight (no vmcnt(0))
+LC_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Internal launcher shared by the GEMM-shaped fused kernels (gemm.hip).
 int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,

@@ -364,31 +364,64 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
   for (int i = 0; i < P; ++i)
     if (i < n) dma_block(blk + i * gridDim.x, i);
   const float inv = 1.0f / keep;
+  // Every LDS access in the loop is inline asm and every barrier a raw one (lds_barrier): hipcc
+  // puts vmcnt(0) in front of __syncthreads() and of any plain access that may alias the ring
+  // (the whole smem array), which drained the two blocks in flight at each of them.
+  const uint32_t lds0 = lds_addr(smem);
+  constexpr int GK = 4, NG = 2 * ND / GK;  // phase-1 fragment reads in groups, one group ahead
+  static_assert(NG * GK == 2 * ND, "phase-1 groups");
 #pragma unroll 1
   for (int i = 0; i < n; ++i, blk += gridDim.x) {
     const int slot = i % AD_NS;
     // block i's DMA landed; the barrier also retires every wave's use of the slot the next DMA
     // overwrites (block i-1's) and of the dpre image
     wait_vm_dyn(min(P - 1, n - 1 - i) * LP + min(i, P) * SP);
-    __syncthreads();
+    lds_barrier();
     if (i + P < n) dma_block(blk + P * gridDim.x, (i + P) % AD_NS);
-    char* xs = smem + Lay::X0 + slot * Lay::XB;
-    const char* hs = smem + Lay::H0 + slot * Lay::HB;
+    const uint32_t xs = lds0 + Lay::X0 + slot * Lay::XB;
+    const uint32_t hs = lds0 + Lay::H0 + slot * Lay::HB;
+    const uint32_t s0 = lds0 + Lay::S0;
+    // an opaque copy of t per block: the LDS addresses are recomputed (a few VALU) instead of
+    // being hoisted out of the loop as ~30 loop-invariant registers (the ND = 12 walker spilled)
+    int tq = t;
+    asm volatile("" : "+v"(tq));
     {
       // phase 1: lane holds dpre^T[j = 16 nt1 + 4g + r][m = 16 mt1 + t]
-      const int row = 16 * mt1 + t, m = blk * AD_R + row;
-      const char* xrow = xs + row * (D * 2);
+      const int row = 16 * mt1 + tq, m = blk * AD_R + row;
+      const uint32_t xrow = xs + row * (D * 2);
+      // unit ks*4 + g swizzled by t (< 16): ((ks & 3) * 4 + g) ^ t, + 16 units per 4 k-slices,
+      // so four base addresses and the instruction's offset field cover all 2 ND reads
+      uint32_t xa[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xa[q] = xrow + ((q * 4 + g) ^ tq) * 16;
+      bf16x8 fb[2][GK];
+      auto rd = [&](int grp, bf16x8* dst) {
+#pragma unroll
+        for (int e = 0; e < GK; ++e) {
+          const int ks = grp * GK + e;
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(dst[e]) : "v"(xa[ks & 3]), "i"((ks >> 2) * 256));
+        }
+      };
+      rd(0, fb[0]);
       f32x4 a1 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2 * ND; ++ks) {
-        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(xrow + ad_swz(t, ks * 4 + g) * 16);
-        a1 = mfma16(wu[ks], fb, a1);
-        // at most 6 fragment reads hoisted ahead (the weights already hold 144 registers)
-        if (ks % 6 == 5) __builtin_amdgcn_sched_barrier(0);
+      for (int grp = 0; grp < NG; ++grp) {
+        if (grp + 1 < NG) {
+          rd(grp + 1, fb[(grp + 1) & 1]);
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(GK) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < GK; ++e) a1 = mfma16(wu[grp * GK + e], fb[grp & 1][e], a1);
       }
       // EPI_AD_MASK: v = acc * scale (+ no bias); (h > 0) ? v / keep : 0
       const int col = 16 * nt1 + 4 * g;
-      const uint2 hb = *reinterpret_cast<const uint2*>(hs + row * 128 + col * 2);
+      uint2 hb;
+      asm volatile("ds_read_b64 %0, %1" : "=v"(hb) : "v"(hs + row * 128 + col * 2));
+      lds_wait0();
       const uint32_t hh[2] = {hb.x, hb.y};
       float o[4];
 #pragma unroll
@@ -400,54 +433,68 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
       const uint2 ob = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
       if (m < M) *reinterpret_cast<uint2*>(dpre + (long)m * AD_H + col) = ob;
       if constexpr (DZ)
-        *reinterpret_cast<uint2*>(smem + Lay::S0 + row * 128 + ad_swz_s(row, col >> 3) * 16 +
-                                  (col & 7) * 2) = ob;
+        asm volatile("ds_write_b64 %0, %1"
+                     :: "v"(s0 + row * 128 + ad_swz_s(row, col >> 3) * 16 + (col & 7) * 2), "v"(ob)
+                     : "memory");
     }
     if constexpr (DZ) {
-      __syncthreads();  // the whole dpre block is in LDS; phase 1's g reads are done
+      lds_barrier();  // the whole dpre block is in LDS; phase 1's g reads are done
 #pragma unroll
       for (int mt = 0; mt < AD_MT; ++mt) {
-        const int row = 16 * mt + t;
+        const int row = 16 * mt + tq;
         bf16x8 fs[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fs[ks] = *reinterpret_cast<const bf16x8*>(smem + Lay::S0 + row * 128 +
-                                                    ad_swz_s(row, ks * 4 + g) * 16);
-        char* xrow = xs + row * (D * 2);
+          asm volatile("ds_read_b128 %0, %1"
+                       : "=v"(fs[ks]) : "v"(s0 + row * 128 + ad_swz_s(row, ks * 4 + g) * 16));
+        const uint32_t xrow = xs + row * (D * 2);
         constexpr int JH = NT2 % 2 == 0 ? NT2 / 2 : NT2;  // tiles in flight (register budget)
 #pragma unroll
         for (int j0 = 0; j0 < NT2; j0 += JH) {
-        f32x4 a2[NT2];
+          // g values of this lane's JH tiles, read while the MFMAs run
+          uint2 gb[JH];
 #pragma unroll
-        for (int j = j0; j < j0 + JH; ++j) {
-          a2[j] = mfma16(wd[j][0], fs[0], f32x4{0.f, 0.f, 0.f, 0.f});
-          a2[j] = mfma16(wd[j][1], fs[1], a2[j]);
-        }
+          for (int j = 0; j < JH; ++j) {
+            const int nn = (w * NT2 + j0 + j) * 16 + 4 * g;
+            asm volatile("ds_read_b64 %0, %1"
+                         : "=v"(gb[j]) : "v"(xrow + ad_swz(tq, nn >> 3) * 16 + (nn & 7) * 2));
+          }
+          lds_wait0();
+          f32x4 a2[JH];
 #pragma unroll
-        for (int j = j0; j < j0 + JH; ++j) {
-          // EPI_AD_ADD: g + acc; lane holds dz[m][n = 16 (w NT2 + j) + 4g + r], written over its
-          // own g values in the image (each element is read and rewritten by the same lane)
-          const int n = (w * NT2 + j) * 16 + 4 * g;
-          uint2* gp = reinterpret_cast<uint2*>(xrow + ad_swz(t, n >> 3) * 16 + (n & 7) * 2);
-          const uint2 gb = *gp;
-          const uint32_t gg[2] = {gb.x, gb.y};
-          float o[4];
+          for (int j = 0; j < JH; ++j) {
+            a2[j] = mfma16(wd[j0 + j][0], fs[0], f32x4{0.f, 0.f, 0.f, 0.f});
+            a2[j] = mfma16(wd[j0 + j][1], fs[1], a2[j]);
+          }
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            o[r] = bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff)) + (a2[j][r] * 1.0f + 0.0f);
-          *gp = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
-        }
+          for (int j = 0; j < JH; ++j) {
+            // EPI_AD_ADD: g + acc; lane holds dz[m][n = 16 (w NT2 + j) + 4g + r], written over its
+            // own g values in the image (each element is read and rewritten by the same lane)
+            const int nn = (w * NT2 + j0 + j) * 16 + 4 * g;
+            const uint32_t gg[2] = {gb[j].x, gb[j].y};
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              o[r] = bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff)) + (a2[j][r] * 1.0f + 0.0f);
+            const uint2 ob = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+            asm volatile("ds_write_b64 %0, %1"
+                         :: "v"(xrow + ad_swz(tq, nn >> 3) * 16 + (nn & 7) * 2), "v"(ob) : "memory");
+          }
         }
       }
-      __syncthreads();  // the dz block is complete in the image
+      lds_barrier();  // the dz block is complete in the image
       // whole-row stores: wave w writes the image's 1-KiB pieces w*XP .. (16 B per lane)
+      uint4 v[XP];
+#pragma unroll
+      for (int i2 = 0; i2 < XP; ++i2)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(v[i2]) : "v"(xs + (w * XP + i2) * 1024 + lane * 16));
+      lds_wait0();
 #pragma unroll
       for (int i2 = 0; i2 < XP; ++i2) {
         const int piece = w * XP + i2, u = piece * 64 + lane;
         const int row = u / RU, cu = ad_swz(row, u % RU);
         const int m = blk * AD_R + row;
-        const uint4 v = *reinterpret_cast<const uint4*>(xs + piece * 1024 + lane * 16);
-        if (m < M) *reinterpret_cast<uint4*>(dz + (long)m * ldz + cu * 8) = v;
+        if (m < M) *reinterpret_cast<uint4*>(dz + (long)m * ldz + cu * 8) = v[i2];
       }
     }
   }
@@ -513,7 +560,7 @@ int grid_for(long work, int block) {
 }
 
 // ---------------------------------------------------------------- LoRA gradients, one pass
-// Rank-r (r <= 16) LoRA gradients of one projection site (lora.py:838-839 / 1073-1074 autograd):
+// Rank-r (r <= 4) LoRA gradients of one projection site (lora.py:838-839 / 1073-1074 autograd):
 //   XA = X A^T [M, r],  dYB = dY B [M, r],  dB[N, r] += s dY^T XA,  dA[r, K] += s dYB^T X
 // reading X [M, K] and dY [M, N] ONCE (the four-GEMM form streams each of them twice). Rows are
 // independent, so a 32-row block b needs only its own rows: X_b (32 x K, whole, in LDS) gives
@@ -541,10 +588,11 @@ struct LoraGeom {
   static constexpr int RED_OFF = RING_OFF + 3 * CHUNK;
   static constexpr int XAT_OFF = RED_OFF + RED;   // bf16 [16][32]
   static constexpr int DYBT_OFF = XAT_OFF + 1024;
-  static constexpr int BYTES = DYBT_OFF + 1024;
+  static constexpr int BT_OFF = DYBT_OFF + 1024;  // B^T rows 0..3 (r <= 4), bf16 [4][N]
+  static constexpr int BYTES = BT_OFF + 4 * NC * 128 * 2;
   static constexpr int XKS = KT / 8;              // XA k-steps per wave
   static constexpr int DAT = KT * 2 / 8;          // dA 16-column tiles per wave
-  // walker slot: dB [N][r] then dA [r][K] (r <= 16, only the real rank is stored)
+  // walker slot: dB [N][r] then dA [r][K] (only the real rank is stored)
 };
 
 LC_DEV void vm_wait_n(int n) {
@@ -597,15 +645,37 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
     const int m = min(blk_row(i) + row, M - 1);
     glds16(dY + (long)m * ldy + c * 128 + cc * 8, dst + wave * 1024);
   };
+  // LDS reads of the DMA'd images as inline asm (a plain read of an LDS-DMA target makes hipcc
+  // wait vmcnt(0) first — it cannot tell the slot apart from the ones in flight — which drained
+  // the ring once per chunk); each use follows an explicit lgkmcnt wait + sched_barrier.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   // row read (A operand): row `row` (lane t's), 16-B chunk `ch` of an image with ROWB-byte rows
-  auto row_frag = [&](const char* img, int rowb, int row, int ch) {
+  auto row_frag = [&](uint32_t img, int rowb, int row, int ch) {
     const int u = (ch >> 1) ^ swz_w(row);
-    return *reinterpret_cast<const bf16x8*>(img + row * rowb + u * 32 + (ch & 1) * 16);
+    bf16x8 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(img + row * rowb + u * 32 + (ch & 1) * 16));
+    return v;
+  };
+  // transposed read: tr_frag's operand (rows row, row + 4 at column col) by two ds_read_b64_tr_b16
+  auto tr_frag_asm = [&](uint32_t img, int rowb, int row, int col) {
+    auto addr = [&](int r) {
+      const int byte = col * 2;
+      const int u = (byte >> 5) ^ swz_w(r);
+      return img + r * rowb + u * 32 + (byte & 31);
+    };
+    bf16x4 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(addr(row)));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(addr(row + 4)));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  auto lgkm0 = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
   };
 
-  // per-walker constant fragments: A rows (XA's B operand) for this wave's k-steps, B^T rows
-  // (dYB's B operand) for this wave's k-step of every chunk
-  bf16x8 af[G::XKS], bf[NC];
+  // per-walker constant fragments: A rows (XA's B operand) for this wave's k-steps; B^T rows
+  // (dYB's B operand) are read per chunk from an LDS copy of its r <= 4 nonzero rows
+  bf16x8 af[G::XKS];
   // (inline-asm loads: hipcc would otherwise wait vmcnt(0) — draining the LDS-DMA ring — at
   // every use inside the loop; the explicit wait below retires them before the first DMA)
 #pragma unroll
@@ -613,12 +683,15 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
     asm volatile("global_load_dwordx4 %0, %1, off"
                  : "=v"(af[k])
                  : "v"(apad + (long)t * lda + (wave * G::XKS + k) * 32 + g * 8));
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-    asm volatile("global_load_dwordx4 %0, %1, off"
-                 : "=v"(bf[c])
-                 : "v"(btpad + (long)t * ldbt + c * 128 + (wave >> 1) * 32 + g * 8));
+  {
+    uint4* bt_l = reinterpret_cast<uint4*>(smem + G::BT_OFF);
+    for (int e = tid; e < 4 * NC * 128 / 8; e += 512) {
+      const int row = e / (NC * 16), c8 = e % (NC * 16);
+      bt_l[e] = *reinterpret_cast<const uint4*>(btpad + (long)row * ldbt + c8 * 8);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the B^T copy (no LDS-DMA in flight yet)
   // LDS hand-offs between waves with LDS-DMA in flight: a raw barrier behind lgkmcnt(0)
   // (__syncthreads() would wait vmcnt(0) and drain the ring)
   auto lds_barrier = [] {
@@ -649,15 +722,20 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
     // X_i landed: younger ops are the two ring pieces issued after it
     vm_wait_n(NC > 1 ? 2 : 1);
     __builtin_amdgcn_s_barrier();
-    const char* ximg = smem + G::X_OFF + (i & 1) * G::XIMG;
+    const uint32_t ximg = lds0 + G::X_OFF + (i & 1) * G::XIMG;
     // ---- XA_i partial: wave's k-steps, both 16-row subtiles
     {
       f32x4 xa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int k = 0; k < G::XKS; ++k)
+      for (int k = 0; k < G::XKS; ++k) {
+        bf16x8 xf[2];
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
-          xa[sub] = mfma16(row_frag(ximg, XROW, sub * 16 + t, (wave * G::XKS + k) * 4 + g), af[k], xa[sub]);
+          xf[sub] = row_frag(ximg, XROW, sub * 16 + t, (wave * G::XKS + k) * 4 + g);
+        lgkm0();
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) xa[sub] = mfma16(xf[sub], af[k], xa[sub]);
+      }
       // lane holds XA[m = sub*16 + 4g + rr][r = t]
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -692,11 +770,19 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
         if (nc < NC) dma_c(i, nc, nq);
         else if (more && nc - NC < NC) dma_c(i + 1, nc - NC, nq);
       }
-      const char* cimg = smem + G::RING_OFF + slot * G::CHUNK;
+      const uint32_t cimg = lds0 + G::RING_OFF + slot * G::CHUNK;
+      bf16x8 bfc;  // B^T[r = t][chunk c, k-step ks, 8g ..]: rows >= 4 are zero (r <= 4)
+      asm volatile("ds_read_b128 %0, %1"
+                   : "=v"(bfc)
+                   : "v"(lds0 + G::BT_OFF + ((t & 3) * NC * 128 + c * 128 + ks * 32 + 8 * g) * 2));
+      const bf16x8 dya = row_frag(cimg, 256, sub * 16 + t, ks * 4 + g);
+      const bf16x8 dyt = tr_frag_asm(cimg, 256, 8 * g + (t >> 2), wave * 16 + (t & 3) * 4);
+      lgkm0();
+      if (t >= 4) bfc = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       // dYB partial: rows sub*16 + t, k-step ks of this chunk
-      dyb = mfma16(row_frag(cimg, 256, sub * 16 + t, ks * 4 + g), bf[c], dyb);
+      dyb = mfma16(dya, bfc, dyb);
       // dB tile `wave` of this chunk: A = dY^T (transposed reads), B = XA
-      accB[c] = mfma16(tr_frag<256>(cimg, 8 * g + (t >> 2), wave * 16 + (t & 3) * 4), xaf, accB[c]);
+      accB[c] = mfma16(dyt, xaf, accB[c]);
       slot = slot == 2 ? 0 : slot + 1;
     }
     // ---- dYB_i: sum the 4 waves of each subtile (each did a quarter of the k-steps)
@@ -714,8 +800,13 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
     // ---- dA += dYB_i^T X_i: A = dYB^T rows, B = X_i columns (transposed reads)
     const bf16x8 dyf = *reinterpret_cast<const bf16x8*>(dybt + t * 32 + g * 8);
 #pragma unroll
-    for (int j = 0; j < G::DAT; ++j)
-      accA[j] = mfma16(dyf, tr_frag<XROW>(ximg, 8 * g + (t >> 2), (wave * G::DAT + j) * 16 + (t & 3) * 4), accA[j]);
+    for (int j = 0; j < G::DAT; j += 2) {
+      const bf16x8 x0 = tr_frag_asm(ximg, XROW, 8 * g + (t >> 2), (wave * G::DAT + j) * 16 + (t & 3) * 4);
+      const bf16x8 x1 = tr_frag_asm(ximg, XROW, 8 * g + (t >> 2), (wave * G::DAT + j + 1) * 16 + (t & 3) * 4);
+      lgkm0();
+      accA[j] = mfma16(dyf, x0, accA[j]);
+      accA[j + 1] = mfma16(dyf, x1, accA[j + 1]);
+    }
   }
   // walker partial: dB [N][r] (lane: rows n = c*128 + wave*16 + 4g + rr, column t < r), dA [r][K]
   // (lane: rows 4g + rr < r, column k = (wave*DAT + j)*16 + t)
@@ -778,27 +869,43 @@ lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats
 //   y     = LN(x_out) * gamma + beta               (bf16, the next GEMM's A operand; mean, rstd saved)
 // Separately these are two skinny GEMM launches and a LayerNorm launch that re-reads x_out
 // (and z twice); here z, resid and x_out each cross HBM once. 16-row blocks; one persistent
-// 8-wave workgroup per CU; z of the next block comes by LDS-DMA and resid by (inline-asm) loads
-// while the current block computes. Both weights live in registers as MFMA fragments: the down
+// 8-wave workgroup per CU. Both weights live in registers as MFMA fragments: the down
 // projection splits K = D over the waves (partials summed through LDS), the up projection gives
 // each wave D/8 output columns of all 16 rows. The row statistics of the LayerNorm (two-pass:
 // mean, then the mean of squared deviations, as ln_fwd_kernel) are summed over the waves in LDS.
 // The dropout mask is drop_mul(seed, row, j) — the EPI_AD_DOWN epilogue's — so the forward is
 // the separate path's, and the backward regenerates the same mask.
+// Streaming: z and resid arrive by LDS-DMA. resid (the larger stream) is double-buffered and
+// issued a whole block ahead, at the top of the block before; z is single-buffered and issued as
+// soon as the current block's z has been read (after the down projection, whose operands and the
+// epilogue's z values are read first), so both have most of a block of lead time. The only VMEM
+// instructions inside a block are those DMAs and the stores, and the wait at the top of a block
+// is COUNTED: the stores issued after the last DMA stay in flight while the next block computes.
+// Down projection: wave w computes the 16 bottleneck columns 16 (w & 3) over the K half (w >> 2),
+// so the cross-wave sum is one partial per output (4 KiB of LDS instead of eight).
 template <int D>
 struct AdLnLay {
   static constexpr int ZROW = D * 2;                 // z image row bytes
   static constexpr int ZIMG = 16 * ZROW;             // one 16-row z block
   static constexpr int ZP = ZIMG / 1024 / 8;         // z DMA pieces per wave
-  static constexpr int Z_OFF = 0;                    // two z buffers
-  static constexpr int RED_OFF = 2 * ZIMG;           // [8][16][64] f32 down partials
-  static constexpr int H_OFF = RED_OFF + 8 * 16 * 64 * 4;   // h block bf16 [16][64]
+  static constexpr int XIMG = 16 * D * 4;            // one 16-row resid block (f32, plain rows)
+  static constexpr int XP = XIMG / 1024 / 8;         // resid DMA pieces per wave
+  static constexpr int Z_OFF = 0;                    // one z buffer
+  static constexpr int X_OFF = ZIMG;                 // two resid buffers
+  static constexpr int RED_OFF = X_OFF + 2 * XIMG;   // [16][64] f32 down partials (K half 1)
+  static constexpr int H_OFF = RED_OFF + 16 * 64 * 4;       // h block bf16 [16][64]
   static constexpr int ST_OFF = H_OFF + 16 * 64 * 2;        // [2][8][16] f32 row sums
-  static constexpr int PRM_OFF = ST_OFF + 2 * 8 * 16 * 4;   // bu, gamma, beta f32 [3][D]
-  static constexpr int BYTES = PRM_OFF + 3 * D * 4;
-  static constexpr int KS = D / 32 / 8;              // down-projection k-steps per wave
+  static constexpr int PRM_OFF = ST_OFF + 2 * 8 * 16 * 4;   // bu, gamma, beta [3][D], bd [64] f32
+  static constexpr int BYTES = PRM_OFF + (3 * D + 64) * 4;
+  static constexpr int KS = D / 32 / 2;              // down-projection k-steps per wave (K half)
   static constexpr int NU = D / 8 / 16;              // up-projection 16-column tiles per wave
+  static_assert(BYTES <= 160 * 1024, "LDS");
 };
+
+template <int N>
+LC_DEV void vmcnt_le() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 template <int D>
 __global__ void __launch_bounds__(512, 1)
@@ -816,6 +923,7 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, t = lane & 15;
+  const int nd = wave & 3, kh = wave >> 2;  // down projection: column tile, K half
   const int nblk = (M + 15) / 16;
   if ((int)blockIdx.x >= nblk) return;
   if (seed_dev) seed += *seed_dev * 0xD1B54A32D192ED03ull;
@@ -828,18 +936,17 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     prm[D + e] = gamma[e];
     prm[2 * D + e] = beta[e];
   }
+  if (tid < 64) prm[3 * D + tid] = bd[tid];
   // weights as fragments (inline-asm loads: invisible to hipcc's vmcnt bookkeeping, retired
   // by the explicit wait below before any LDS-DMA is in flight)
-  //   down: B[k][j] = Wd[j][k], lane (t, g): Wd row (16 n + t), k = (wave KS + ks) 32 + 8g ..
+  //   down: B[k][j] = Wd[j][k], lane (t, g): Wd row (16 nd + t), k = (kh KS + ks) 32 + 8g ..
   //   up:   B[k][j] = Wu[j][k], lane (t, g): Wu row (wave D/8 + 16 u + t), k = 32 ks + 8g ..
-  bf16x8 wdf[KS][4], wuf[NU][2];
+  bf16x8 wdf[KS], wuf[NU][2];
 #pragma unroll
   for (int k = 0; k < KS; ++k)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-      asm volatile("global_load_dwordx4 %0, %1, off"
-                   : "=v"(wdf[k][n])
-                   : "v"(Wd + (long)(16 * n + t) * D + (wave * KS + k) * 32 + 8 * g));
+    asm volatile("global_load_dwordx4 %0, %1, off"
+                 : "=v"(wdf[k])
+                 : "v"(Wd + (long)(16 * nd + t) * D + (kh * KS + k) * 32 + 8 * g));
 #pragma unroll
   for (int u = 0; u < NU; ++u)
 #pragma unroll
@@ -849,10 +956,10 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
                    : "v"(Wu + (long)(wave * (D / 8) + 16 * u + t) * 64 + 32 * k + 8 * g));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // z block b -> buffer buf: 1-KiB pieces, lane -> (row, 16-B position) inverting the 32-B
+  // z block b -> the z buffer: 1-KiB pieces, lane -> (row, 16-B position) inverting the 32-B
   // unit swizzle (swz_w: conflict-free row reads and 8-B epilogue reads)
-  auto dma_z = [&](int b, int buf) {
-    char* dst = smem + L::Z_OFF + buf * L::ZIMG;
+  auto dma_z = [&](int b) {
+    char* dst = smem + L::Z_OFF;
     const int r0 = b * 16;
 #pragma unroll
     for (int pp = 0; pp < L::ZP; ++pp) {
@@ -864,103 +971,142 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
       glds16(z + (long)m * ldz + c * 8, dst + piece * 1024);
     }
   };
-  auto zaddr = [&](const char* img, int row, int byte) {  // byte offset within the row
+  // resid block b -> resid buffer buf, plain row-major [16][D] f32 (the epilogue's 16-B reads of
+  // 16 rows at one column are spread by the row stride D*4 = 3 / 2 KiB: 2-way at worst)
+  auto dma_x = [&](int b, int buf) {
+    char* dst = smem + L::X_OFF + buf * L::XIMG;
+#pragma unroll
+    for (int pp = 0; pp < L::XP; ++pp) {
+      const int piece = wave * L::XP + pp;
+      const int idx = piece * 64 + lane;
+      const int row = idx / (D / 4), c4 = idx % (D / 4);
+      const int m = min(b * 16 + row, M - 1);
+      glds16(resid + (long)m * ldx + c4 * 4, dst + piece * 1024);
+    }
+  };
+  const uint32_t lds0 = lds_addr(smem);
+  auto zaddr = [&](int row, int byte) {  // LDS address of z image byte `byte` of row `row`
     const int u = (byte >> 5) ^ swz_w(row);
-    return img + row * L::ZROW + u * 32 + (byte & 31);
+    return lds0 + L::Z_OFF + row * L::ZROW + u * 32 + (byte & 31);
   };
-  // resid of block b for this lane's outputs: row t, columns wave D/8 + 16 u + 4 g .. +3
-  auto load_x = [&](int b, f32x4 (&xr)[NU]) {
-    const int m = min(b * 16 + t, M - 1);
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-      asm volatile("global_load_dwordx4 %0, %1, off"
-                   : "=v"(xr[u])
-                   : "v"(resid + (long)m * ldx + wave * (D / 8) + 16 * u + 4 * g));
-  };
-  auto lds_barrier = [] {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
+  // stores issued after the last DMA of a full block, per wave: h (waves 0-1), x_out and y (NU
+  // each), mean and rstd (wave 0)
+  const int tail = 2 * NU + (wave < 2 ? 1 : 0) + (wave == 0 ? 2 : 0);
 
-  f32x4 xa[NU], xb[NU];
   int b = blockIdx.x;
-  dma_z(b, 0);
-  load_x(b, xa);
-  // buf: this walker's iteration parity (the z double buffer; blocks b and b + gridDim.x can
-  // have the same index parity)
-  auto body = [&](int b, int buf, f32x4 (&xr)[NU], f32x4 (&xn)[NU]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // z_b, resid_b, and the last block's stores
-    __syncthreads();  // also publishes prm on the first block
-    const int bn = b + gridDim.x;
-    if (bn < nblk) {
-      dma_z(bn, buf ^ 1);  // the other buffer: read by the previous block only
-      load_x(bn, xn);
-    }
-    const char* zi = smem + L::Z_OFF + buf * L::ZIMG;
+  dma_x(b, 0);
+  dma_z(b);
+  __syncthreads();  // prm (no LDS-DMA waited on here: the first block's wait comes next)
+  bool prev_full = false;
+#pragma unroll 1
+  for (int k = 0; b < nblk; ++k, b += gridDim.x) {
+    const int buf = k & 1;
     const int r0 = b * 16;
-    // ---- down projection: partial over this wave's KS k-steps, all 64 bottleneck columns
+    // this block's z and resid landed; the previous block's tail stores may stay in flight
+    if (prev_full) {
+      if (tail == 2 * NU + 3) vmcnt_le<2 * NU + 3>();
+      else if (tail == 2 * NU + 1) vmcnt_le<2 * NU + 1>();
+      else vmcnt_le<2 * NU>();
+    } else {
+      vmcnt_le<0>();
+    }
+    lds_barrier();
+    const int bn = b + gridDim.x;
+    if (bn < nblk) dma_x(bn, buf ^ 1);  // the other buffer: read by the previous block only
+    // ---- down projection: this wave's column tile over its K half (A = z rows t)
+    f32x4 pd = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint2 zz[NU];
     {
-      f32x4 pd[4];
+      constexpr int GK = KS / 2;  // two groups of reads, the second in flight under the first's MFMAs
+      bf16x8 za[KS];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) pd[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < KS; ++ks)
+        asm volatile("ds_read_b128 %0, %1"
+                     : "=v"(za[ks]) : "v"(zaddr(t, ((kh * KS + ks) * 32 + 8 * g) * 2)));
+      // the epilogue's z values (row t, this wave's up-projection columns), read now so that the
+      // z buffer is free for the next block's DMA after the barrier below
 #pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const int byte = ((wave * KS + k) * 32 + 8 * g) * 2;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(zaddr(zi, t, byte));
+      for (int u = 0; u < NU; ++u)
+        asm volatile("ds_read_b64 %0, %1"
+                     : "=v"(zz[u]) : "v"(zaddr(t, (wave * (D / 8) + 16 * u + 4 * g) * 2)));
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NU + KS - GK) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) pd[n] = mfma16(a, wdf[k][n], pd[n]);
+      for (int ks = 0; ks < GK; ++ks) pd = mfma16(za[ks], wdf[ks], pd);
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NU) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = GK; ks < KS; ++ks) pd = mfma16(za[ks], wdf[ks], pd);
+    }
+    // lane holds P[m = 4g + rr][j = 16 nd + t] over K half kh
+    if (kh == 1)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[(4 * g + rr) * 64 + 16 * nd + t] = pd[rr];
+    lds_barrier();  // also: every wave's z reads are done (lgkmcnt(0) above the barrier)
+    if (bn < nblk) dma_z(bn);
+    if (kh == 0) {
+      const int j = 16 * nd + t;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = 4 * g + rr;
+        float v = pd[rr] + red[m * 64 + j];
+        v = fmaxf(v + prm[3 * D + j], 0.f) * drop_mul(seed, (long)(r0 + m), j, keep);
+        hs[m * 64 + j] = f2bf(v);
       }
-      // lane holds P[m = 4g + rr][j = 16n + t]
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) red[(wave * 16 + 4 * g + rr) * 64 + 16 * n + t] = pd[n][rr];
     }
     lds_barrier();
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {  // 1024 outputs, 2 per thread
-      const int e = tid + 512 * q, m = e >> 6, j = e & 63;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) v += red[(w * 16 + m) * 64 + j];
-      v = fmaxf(v + bd[j], 0.f) * drop_mul(seed, (long)(r0 + m), j, keep);
-      const bf16_t hb = f2bf(v);
-      hs[m * 64 + j] = hb;
-      if (r0 + m < M) hout[(long)(r0 + m) * 64 + j] = hb;
+    // (every LDS read from here on is inline asm: hipcc treats a plain read as possibly aliasing
+    // the LDS-DMA in flight and waits vmcnt(0) first)
+    const uint32_t hl = lds0 + L::H_OFF;
+    if (wave < 2) {  // the h block (2 KiB, contiguous in hout) as 16-B row pieces
+      const int e = tid;  // 128 pieces: row e >> 3, 8 columns (e & 7) * 8
+      uint4 v;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(hl + e * 16));
+      lds_wait0();
+      if (r0 + (e >> 3) < M) *reinterpret_cast<uint4*>(hout + (long)r0 * 64 + e * 8) = v;
     }
-    lds_barrier();
     // ---- up projection: rows t of the block (A = h), this wave's D/8 columns (B = Wu)
-    const bf16x8 ha0 = *reinterpret_cast<const bf16x8*>(hs + t * 64 + 8 * g);
-    const bf16x8 ha1 = *reinterpret_cast<const bf16x8*>(hs + t * 64 + 32 + 8 * g);
+    bf16x8 ha0, ha1;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(ha0) : "v"(hl + (t * 64 + 8 * g) * 2));
+    asm volatile("ds_read_b128 %0, %1" : "=v"(ha1) : "v"(hl + (t * 64 + 32 + 8 * g) * 2));
     f32x4 xo[NU];
     float s1 = 0.f;
+    // resid of this lane's outputs from the DMA'd image
+    f32x4 xr4[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int col = wave * (D / 8) + 16 * u + 4 * g;
+      asm volatile("ds_read_b128 %0, %1"
+                   : "=v"(xr4[u]) : "v"(lds0 + L::X_OFF + buf * L::XIMG + (t * D + col) * 4));
+    }
+    lds_wait0();
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       f32x4 acc = mfma16(wuf[u][0], ha0, f32x4{0.f, 0.f, 0.f, 0.f});
       acc = mfma16(wuf[u][1], ha1, acc);
       // lane holds U[m = t][n = col + rr], col = wave D/8 + 16u + 4g (the swapped layout)
       const int col = wave * (D / 8) + 16 * u + 4 * g;
-      const uint2 zz = *reinterpret_cast<const uint2*>(zaddr(zi, t, col * 2));
-      const float zf[4] = {bf2f(zz.x & 0xffff), bf2f(zz.x >> 16), bf2f(zz.y & 0xffff), bf2f(zz.y >> 16)};
+      const float zf[4] = {bf2f(zz[u].x & 0xffff), bf2f(zz[u].x >> 16), bf2f(zz[u].y & 0xffff),
+                           bf2f(zz[u].y >> 16)};
+      const f32x4 xr = xr4[u];
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const float v = acc[rr] + prm[col + rr];
-        xo[u][rr] = xr[u][rr] + zf[rr] + scale * v;
+        xo[u][rr] = xr[rr] + zf[rr] + scale * v;
         s1 += xo[u][rr];
       }
-    }
-    const bool live = r0 + t < M;
-    if (live) {
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-        *reinterpret_cast<f32x4*>(xout + (long)(r0 + t) * ldx + wave * (D / 8) + 16 * u + 4 * g) = xo[u];
     }
     // ---- LayerNorm of the 16 rows: sums over the 4 lanes of a row, then over the waves
     s1 += __shfl_xor(s1, 16);
     s1 += __shfl_xor(s1, 32);
     if (g == 0) st[wave * 16 + t] = s1;
     lds_barrier();
+    const bool live = r0 + t < M;
+    if (live) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        *reinterpret_cast<f32x4*>(xout + (long)(r0 + t) * ldx + wave * (D / 8) + 16 * u + 4 * g) = xo[u];
+    }
     float mean = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) mean += st[w * 16 + t];
@@ -996,11 +1142,8 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
         rstd_out[r0 + t] = rstd;
       }
     }
-  };
-#pragma unroll 1
-  for (; b < nblk; b += 2 * gridDim.x) {
-    body(b, 0, xa, xb);
-    if (b + (int)gridDim.x < nblk) body(b + gridDim.x, 1, xb, xa);
+    // st is rewritten by the next block only after its first two barriers
+    prev_full = r0 + 16 <= M;
   }
 }
 
@@ -1063,7 +1206,7 @@ int lc_lora_grad(hipStream_t st, int M, int N, int K, int r, const void* dY, lon
 int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
                     const void* X, long ldx, const void* apad, long lda, const void* btpad,
                     long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes) {
-  LC_CHECK_ARG(M > 0 && r >= 1 && r <= 16 && dY && X && apad && btpad && dA && dB && ws);
+  LC_CHECK_ARG(M > 0 && r >= 1 && r <= 4 && dY && X && apad && btpad && dA && dB && ws);
   LC_CHECK_ARG(ldy % 8 == 0 && ldx % 8 == 0 && lda % 8 == 0 && ldbt % 8 == 0);
   LC_CHECK_ARG(ldy >= N && ldx >= K && lda >= K && ldbt >= N);
   const int nblk = (M + 31) / 32;

@@ -561,7 +561,7 @@ class BlockStack:
         M = dY.shape[0]
         r, K = A.shape
         N = B.shape[0]
-        if self.LORA_1P and (K, N) in ((768, 2304), (768, 768), (512, 1536), (512, 512)):
+        if self.LORA_1P and r <= 4 and (K, N) in ((768, 2304), (768, 768), (512, 1536), (512, 512)):
             with self._side():
                 ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, self._grad(grads, A),
                                  self._grad(grads, B))
