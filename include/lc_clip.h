@@ -236,6 +236,15 @@ int lc_merge_weight(hipStream_t stream, int N, int K, int r, const float* W, con
 int lc_cast_weights_bf16(hipStream_t stream, int n, const float* const* W, const int* N,
                          const int* K, void* const* out, void* const* outT);
 
+/* Batched merges: lc_merge_weight for n <= LC_CAST_MAX items in one launch (host arrays; A[i] /
+ * B[i] NULL with r[i] == 0 for a plain cast). The LoRA towers re-merge every block's in-proj and
+ * out-proj weights and re-stage the bf16 A / B^T gradient operands after each optimizer step:
+ * 6 items per block, 72 launches of 3-9 us on the critical path before.
+ * Replaces: the per-step LoRA residual merges of lora.py:838-839, 1073-1074 (as lc_merge_weight). */
+int lc_merge_weights_bf16(hipStream_t stream, int n, const float* const* W, const float* const* A,
+                          const float* const* B, const int* r, const float* scaling, const int* N,
+                          const int* K, void* const* out, void* const* outT);
+
 /* dB[N,r] += scaling * dY^T (X A^T);  dA[r,K] += scaling * (dY B)^T X   (r == 4).
  * Replaces: autograd of the two F.linear LoRA products (lora.py:838-839, 1073-1074). */
 int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,

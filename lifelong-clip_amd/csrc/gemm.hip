@@ -1733,7 +1733,12 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
   ep.group_m = group_m(N);
   const int tiles = ((M + 255) / 256) * (N / 256);
   const int units = K / (FP8 ? 128 : 64);
-  const SplitK sk = plan_split(tiles, units, 8, ws, ws_bytes);
+  // (LC_GEMM_SPLIT_MIN overrides the minimum k-tiles per split-K slice: in-step A/Bs)
+  static const int split_min = [] {
+    const char* e = getenv("LC_GEMM_SPLIT_MIN");
+    return e && atoi(e) > 0 ? atoi(e) : 8;
+  }();
+  const SplitK sk = plan_split(tiles, units, split_min, ws, ws_bytes);
   const long ea = FP8 ? 1 : 2;  // bytes per element
   dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
 #define LC_G8_CASE(E)                                                                          \
@@ -1812,7 +1817,12 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     else if (M >= 4096 && N <= 768) tile = 4;
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 289 vs 295 us (bench_gemm.py)
-    if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048) tile = 7;
+    // (LC_GEMM_MUL_W4=0 keeps it on gemm8: in-step A/Bs)
+    static const bool mul_w4 = [] {
+      const char* e = getenv("LC_GEMM_MUL_W4");
+      return !(e && e[0] == '0');
+    }();
+    if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048 && mul_w4) tile = 7;
     // one-k-tile streams (adapter up-projection / input gradient, K = 64): 128x64 tiles keep
     // more rows in flight per CU (tools/bench_adapter_kernels.py: AD_UP 83 -> 77 us, AD_ADD
     // 37 -> 35 us)

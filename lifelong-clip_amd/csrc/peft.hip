@@ -112,18 +112,24 @@ merge_kernel(int N, int K, int r, const float* __restrict__ W, const float* __re
 // Many plain casts in one launch (the adapter weights of every block after each optimizer step:
 // 2 x 2 small matrices per block, 48 launches of ~5 us each on the step's critical path before).
 // blockIdx.y = item, blockIdx.x = 64x64 tile of that item.
+// The same batch form carries LoRA merges (A, B, r, s per item; the LoRA towers' 6 merges per
+// block after each optimizer step).
 struct CastBatch {
   const float* W[LC_CAST_MAX];
+  const float* A[LC_CAST_MAX];
+  const float* B[LC_CAST_MAX];
   bf16_t* out[LC_CAST_MAX];
   bf16_t* outT[LC_CAST_MAX];
-  int N[LC_CAST_MAX], K[LC_CAST_MAX];
+  int N[LC_CAST_MAX], K[LC_CAST_MAX], r[LC_CAST_MAX];
+  float s[LC_CAST_MAX];
 };
+static_assert(sizeof(CastBatch) <= 4096, "kernel argument block");
 __global__ void __launch_bounds__(256) cast_batch_kernel(CastBatch b) {
   const int it = blockIdx.y;
   const int N = b.N[it], K = b.K[it];
   const int tk = (K + 63) / 64;
   if ((int)blockIdx.x >= tk * ((N + 63) / 64)) return;
-  merge_tile(N, K, 0, b.W[it], nullptr, nullptr, 0.f, b.out[it], b.outT[it],
+  merge_tile(N, K, b.r[it], b.W[it], b.A[it], b.B[it], b.s[it], b.out[it], b.outT[it],
              (blockIdx.x / tk) * 64, (blockIdx.x % tk) * 64);
 }
 
@@ -1172,11 +1178,26 @@ int lc_cast_weights_bf16(hipStream_t st, int n, const float* const* W, const int
                          const int* K, void* const* out, void* const* outT) {
   LC_CHECK_ARG(n >= 0 && n <= LC_CAST_MAX && (n == 0 || (W && N && K && out && outT)));
   if (n == 0) return LC_OK;
+  return lc_merge_weights_bf16(st, n, W, nullptr, nullptr, nullptr, nullptr, N, K, out, outT);
+}
+
+int lc_merge_weights_bf16(hipStream_t st, int n, const float* const* W, const float* const* A,
+                          const float* const* B, const int* r, const float* scaling, const int* N,
+                          const int* K, void* const* out, void* const* outT) {
+  LC_CHECK_ARG(n >= 0 && n <= LC_CAST_MAX && (n == 0 || (W && N && K && out && outT)));
+  LC_CHECK_ARG((r == nullptr) == (scaling == nullptr));
+  if (n == 0) return LC_OK;
   CastBatch b{};
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
     LC_CHECK_ARG(W[i] != nullptr && out[i] != nullptr && N[i] > 0 && K[i] > 0);
+    const int ri = r ? r[i] : 0;
+    LC_CHECK_ARG(ri >= 0 && ri <= MERGE_RMAX && (ri == 0 || (A && B && A[i] && B[i])));
     b.W[i] = W[i];
+    b.A[i] = ri ? A[i] : nullptr;
+    b.B[i] = ri ? B[i] : nullptr;
+    b.r[i] = ri;
+    b.s[i] = ri ? scaling[i] : 0.f;
     b.out[i] = static_cast<bf16_t*>(out[i]);
     b.outT[i] = static_cast<bf16_t*>(outT[i]);
     b.N[i] = N[i];

@@ -49,6 +49,7 @@ SIGNATURES = {
     "lc_cast_bf16": [P, c_long, P, P],
     "lc_merge_weight": [P, c_int, c_int, c_int, P, P, P, c_float, P, P],
     "lc_cast_weights_bf16": [P, c_int, P, P, P, P, P],
+    "lc_merge_weights_bf16": [P, c_int, P, P, P, P, P, P, P, P, P],
     "lc_lora_grad": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, c_float, P, P],
     "lc_lora_grad_ws": [P, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_long, P, c_long,
                         c_float, P, P, P, c_long],

@@ -100,7 +100,7 @@ class BlockStack:
             st.peft_key = None
 
     def stage(self):
-        casts = []
+        casts, merges = [], []
         for blk, st in zip(self.blocks, self.staged):
             attn, mlp = blk.attn, blk.mlp
             fkey = _key(attn.in_proj_weight, attn.out_proj.weight, mlp.c_fc.weight, mlp.c_proj.weight)
@@ -127,15 +127,15 @@ class BlockStack:
                             attn.out_proj.lora_A, attn.out_proj.lora_B) + fkey
                 if pkey != st.peft_key:
                     s = attn.scaling
-                    ops.merge_weight(attn.in_proj_weight.detach(), attn.in_proj_weight_lora_A.detach(),
-                                     attn.in_proj_weight_lora_B.detach(), s, st.wqkv, st.wqkvT)
-                    ops.merge_weight(attn.out_proj.weight.detach(), attn.out_proj.lora_A.detach(),
-                                     attn.out_proj.lora_B.detach(), s, st.wo, st.woT)
+                    merges.append((attn.in_proj_weight.detach(), attn.in_proj_weight_lora_A.detach(),
+                                   attn.in_proj_weight_lora_B.detach(), s, st.wqkv, st.wqkvT))
+                    merges.append((attn.out_proj.weight.detach(), attn.out_proj.lora_A.detach(),
+                                   attn.out_proj.lora_B.detach(), s, st.wo, st.woT))
                     # bf16 A and B^T zero-padded to 64 rows: operands of the LoRA-gradient GEMMs
                     st.lora_in = self._stage_lora(st, "lora_in", attn.in_proj_weight_lora_A,
-                                                  attn.in_proj_weight_lora_B)
+                                                  attn.in_proj_weight_lora_B, merges)
                     st.lora_out = self._stage_lora(st, "lora_out", attn.out_proj.lora_A,
-                                                   attn.out_proj.lora_B)
+                                                   attn.out_proj.lora_B, merges)
                     st.peft_key = pkey
                     # the fused AdamW bypasses the version counters, so the re-merged weights can
                     # carry the same pkey as before: the epoch is what tells _stage_fp8 to re-quantise
@@ -154,9 +154,14 @@ class BlockStack:
                     casts.append((ad.down_proj.weight.detach(), st.wd, st.wdT))
                     casts.append((ad.up_proj.weight.detach(), st.wu, st.wuT))
                     st.peft_key = pkey
-        # the adapter weights of every block change at each optimizer step: one launch for all
+        # the PEFT weights of every block change at each optimizer step: one launch for all
+        # (LoRA: 6 merges / casts per block, a launch per CAST_MAX items)
         if casts:
             ops.cast_weights(casts)
+        if merges and self.MERGE_BATCH:
+            ops.merge_weights(merges)
+        for item in (merges if not self.MERGE_BATCH else ()):
+            ops.merge_weight(*item)
         if self.precision == "fp8":
             self._stage_fp8()
 
@@ -204,8 +209,9 @@ class BlockStack:
         return ops.gemm_nt(A, getattr(st, name), epi, out0, **kw)
 
     @staticmethod
-    def _stage_lora(st, name, A, B):
-        """(A_pad [64,K], Bt_pad [64,N]) bf16 with rows >= r zero, staged from A [r,K], B [N,r]."""
+    def _stage_lora(st, name, A, B, merges):
+        """(A_pad [64,K], Bt_pad [64,N]) bf16 with rows >= r zero, staged from A [r,K], B [N,r]
+        by two casts appended to `merges` (launched with the block's weight merges)."""
         r, K = A.shape
         N = B.shape[0]
         old = getattr(st, name, None)
@@ -215,8 +221,8 @@ class BlockStack:
                    torch.zeros((64, N), dtype=BF16, device=dev),
                    _empty((N, r), BF16, dev))
         a_pad, bt_pad, scratch = old
-        ops.merge_weight(A.detach(), None, None, 0.0, a_pad[:r])
-        ops.merge_weight(B.detach(), None, None, 0.0, scratch, bt_pad[:r])
+        merges.append((A.detach(), None, None, 0.0, a_pad[:r], None))
+        merges.append((B.detach(), None, None, 0.0, scratch, bt_pad[:r]))
         return old
 
     # ------------------------------------------------------------------ forward
@@ -548,6 +554,8 @@ class BlockStack:
                               self._grad(grads, ad.down_proj.bias))
         return dz
 
+    # LCCLIP_MERGE_BATCH=0: one lc_merge_weight launch per LoRA merge / cast (A/B experiments)
+    MERGE_BATCH = os.environ.get("LCCLIP_MERGE_BATCH", "1") != "0"
     # LCCLIP_LORA_1P=0: the four-GEMM form (A/B experiments)
     LORA_1P = os.environ.get("LCCLIP_LORA_1P", "1") != "0"
 

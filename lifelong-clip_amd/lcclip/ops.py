@@ -288,6 +288,39 @@ def cast_weights(items):
         call("lc_cast_weights_bf16", stream_of(chunk[0][0]), n, ws, Ns, Ks, outs, outTs)
 
 
+def merge_weights(items):
+    """items: [(W f32 [N, K], A f32 [r, K] or None, B f32 [N, r] or None, scaling,
+    out bf16 [N, K], outT bf16 [K, N] or None)] -> out = bf16(W + scaling B A) (and its
+    transpose), one launch per CAST_MAX items (lc_merge_weights_bf16)."""
+    import ctypes
+    for i in range(0, len(items), CAST_MAX):
+        chunk = items[i:i + CAST_MAX]
+        n = len(chunk)
+        for W, A, B, _, out, outT in chunk:
+            if W.dtype != F32 or not W.is_contiguous() or out.dtype != BF16 or not out.is_contiguous():
+                raise ValueError("merge_weights: W must be contiguous f32, out contiguous bf16")
+            if out.shape != W.shape or (outT is not None and (outT.shape != W.shape[::-1]
+                                                              or not outT.is_contiguous())):
+                raise ValueError("merge_weights: shape mismatch")
+            if A is not None:
+                r = A.shape[0]
+                if (A.dtype != F32 or B.dtype != F32 or not A.is_contiguous() or not B.is_contiguous()
+                        or A.shape[1] != W.shape[1] or tuple(B.shape) != (W.shape[0], r) or r > 8):
+                    raise ValueError("merge_weights: A [r, K] / B [N, r] f32 contiguous, r <= 8")
+        P = ctypes.c_void_p
+        ws = (P * n)(*[ptr(c[0]) for c in chunk])
+        As = (P * n)(*[ptr(c[1]) for c in chunk])
+        Bs = (P * n)(*[ptr(c[2]) for c in chunk])
+        rs = (ctypes.c_int * n)(*[0 if c[1] is None else c[1].shape[0] for c in chunk])
+        ss = (ctypes.c_float * n)(*[float(c[3]) for c in chunk])
+        Ns = (ctypes.c_int * n)(*[c[0].shape[0] for c in chunk])
+        Ks = (ctypes.c_int * n)(*[c[0].shape[1] for c in chunk])
+        outs = (P * n)(*[ptr(c[4]) for c in chunk])
+        outTs = (P * n)(*[ptr(c[5]) for c in chunk])
+        call("lc_merge_weights_bf16", stream_of(chunk[0][0]), n, ws, As, Bs, rs, ss, Ns, Ks, outs,
+             outTs)
+
+
 def lora_grad(dY, X, A, B, scaling, dA, dB):
     M, N = dY.shape
     K = X.shape[1]

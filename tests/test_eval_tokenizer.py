@@ -153,3 +153,33 @@ def test_tokenizer_reproduces_token_fixture():
     d = _token_golden()
     for name, ids in d["ids"].items():
         assert [t.sot] + t.encode(d["template"].format(name)) + [t.eot] == ids, name
+
+
+TOKEN_GOLDEN_HF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                               "clip_tokens_cifar100_hf.json")
+
+
+def test_token_fixture_matches_independent_tokenizer():
+    """Runs without /root/reference: every CIFAR-100 prompt row of the build's fixture equals the
+    ids of an independent CLIP BPE implementation (transformers' CLIPTokenizer over the same
+    merges file, tests/golden/make_token_golden_hf.py), so the class-name ids are pinned by more
+    than the build's own tokenizer."""
+    import json
+    d = _token_golden()
+    with open(TOKEN_GOLDEN_HF) as f:
+        hf = json.load(f)["ids"]
+    for name, ids in d["ids"].items():
+        assert hf[d["template"].format(name)] == ids, name
+
+
+@pytest.mark.skipif(not os.path.isfile(BPE), reason="BPE merges file not available")
+def test_tokenizer_matches_independent_tokenizer_free_text():
+    """Free text (punctuation, digits, case, underscores, contractions) through lcclip's BPE vs the
+    independent implementation's committed ids."""
+    import json
+    from lcclip.tokenizer import BPETokenizer
+    t = BPETokenizer(BPE)
+    with open(TOKEN_GOLDEN_HF) as f:
+        hf = json.load(f)["ids"]
+    for text, ids in hf.items():
+        assert [t.sot] + t.encode(text) + [t.eot] == ids, text

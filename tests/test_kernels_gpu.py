@@ -110,7 +110,7 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
-                                   (296 * 256 - 100, 256, 2048)])
+                                   (296 * 256 - 100, 256, 2048), (50432, 768, 768)])
 @pytest.mark.parametrize("tile", [0, 8])
 def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
     from lcclip import _lib
@@ -586,6 +586,37 @@ def test_cast_weights_batch(ops, dev):
         assert torch.equal(out, W.to(BF))
         if outT is not None:
             assert torch.equal(outT, W.t().to(BF))
+
+
+def test_merge_weights_batch(ops, dev):
+    """lc_merge_weights_bf16: LoRA merges (W + s B A, r = 1..4, with and without the transposed
+    copy) and plain casts mixed in one launch, bit-equal to one lc_merge_weight per item and
+    within bf16 rounding of torch fp32; more items than one launch holds (CAST_MAX)."""
+    g = torch.Generator(device=dev).manual_seed(11)
+    items, singles = [], []
+    shapes = [(2304, 768, 4), (768, 768, 4), (4, 768, 0), (768, 4, 0), (1536, 512, 3),
+              (130, 70, 1), (3, 5, 2)] * 10
+    for i, (n, k, r) in enumerate(shapes):
+        W = torch.randn(n, k, device=dev, generator=g)
+        A = torch.randn(r, k, device=dev, generator=g) if r else None
+        B = torch.randn(n, r, device=dev, generator=g) if r else None
+        s = 0.5 + i / len(shapes)
+        out = torch.empty(n, k, device=dev, dtype=BF)
+        outT = torch.empty(k, n, device=dev, dtype=BF) if i % 3 else None
+        items.append((W, A, B, s, out, outT))
+        o1 = torch.empty_like(out)
+        t1 = torch.empty_like(outT) if outT is not None else None
+        ops.merge_weight(W, A, B, s, o1, t1)
+        singles.append((o1, t1))
+    assert len(items) > ops.CAST_MAX
+    ops.merge_weights(items)
+    torch.cuda.synchronize()
+    for (W, A, B, s, out, outT), (o1, t1) in zip(items, singles):
+        assert torch.equal(out, o1)
+        ref = W + (s * B @ A if A is not None else 0)
+        assert (out.float() - ref).abs().max() <= 2 ** -7 * ref.abs().max() + 1e-6
+        if outT is not None:
+            assert torch.equal(outT, t1) and torch.equal(outT, out.t())
 
 
 @pytest.mark.parametrize("M,K,N", [(50432, 768, 2304), (3000 + 17, 768, 768), (770, 512, 1536),
