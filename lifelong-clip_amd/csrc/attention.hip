@@ -319,7 +319,7 @@ attn_bwd_kv_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq
     dsum += __shfl_xor(dsum, 4);
     if (ch == 0) {
       nd_s[r] = -dsum;
-      nlse_s[r] = -lv[i];
+      nlse_s[r] = r < L ? -lv[i] : -1e30f;
     }
   }
   __syncthreads();
@@ -458,6 +458,25 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   const int ch = tid & 7;
   uint4 qv[IT], dv[IT], ov[IT];
   float lv[IT];
+  // Every global access of an item goes through a raw-buffer descriptor over that sequence's L
+  // rows (wave-uniform): rows >= L fall outside it, so their loads return zero and their stores
+  // are dropped by the range check. No branch surrounds a memory op, so hipcc can count vmcnt
+  // across them — with a store under a branch it waits vmcnt(0) at the next use of any earlier
+  // load, i.e. for every store still in flight (the whole store latency once per item).
+  // (ok = false: an empty descriptor — the past-the-end prefetch and the first item's deferred
+  // dQ are issued unconditionally and read zeros / store nothing, so their count never depends
+  // on a branch either)
+  auto rows_rsrc = [&](const void* p, long row0, long row_bytes, bool ok = true) {
+    const uint64_t a = (uint64_t)(static_cast<const char*>(p) + (ok ? row0 * row_bytes : 0));
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int n = __builtin_amdgcn_readfirstlane(ok ? (int)(L * row_bytes) : 0);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+  };
+  auto bld16 = [](__amdgpu_buffer_rsrc_t r, int off) {  // nontemporal (read once)
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
   // Q rows and lse (prefetched during phase 1), dO and O rows (during phase 2: registers). The
   // per-lane row offsets are recomputed from an opaque copy of tid at every call: hoisted out of
   // the item loop they would stay live through both phases (and spill).
@@ -468,22 +487,29 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   };
   auto load_rows = [&](int it_) {
     const int tv = lane_tid();
-    const bf16_t* qb = qkv + (long)(it_ / H) * L * ldq + (it_ % H) * 64 + (tv & 7) * 8;
+    const bool ok = it_ < n_items;
+    const auto rq = rows_rsrc(qkv, (long)(it_ / H) * L, ldq * 2, ok);
+    const auto rl = rows_rsrc(lse, (long)it_ * L, 4, ok);  // this item's L lse values
+    const int cb = ((it_ % H) * 64 + (tv & 7) * 8) * 2;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int r = (tv + i * NTH) >> 3;
-      qv[i] = ld16_or_zero(qb + r * (int)ldq, r < L);
-      lv[i] = (r < L) ? lse[(long)it_ * L + r] : 1e30f;
+      qv[i] = bld16(rq, r * (int)ldq * 2 + cb);
+      // rows >= L read 0 here; the padded-row value (1e30) is substituted where lv is used
+      lv[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, r * 4, 0, 0));
     }
   };
   auto load_o = [&](int it_) {
     const int tv = lane_tid();
-    const long rb = (long)(it_ / H) * L * ldo + (it_ % H) * 64 + (tv & 7) * 8;
+    const bool ok = it_ < n_items;
+    const auto rd = rows_rsrc(dO, (long)(it_ / H) * L, ldo * 2, ok);
+    const auto ro = rows_rsrc(O, (long)(it_ / H) * L, ldo * 2, ok);
+    const int cb = ((it_ % H) * 64 + (tv & 7) * 8) * 2;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int r = (tv + i * NTH) >> 3;
-      dv[i] = ld16_or_zero(dO + rb + r * (int)ldo, r < L);
-      ov[i] = ld16_or_zero(O + rb + r * (int)ldo, r < L);
+      dv[i] = bld16(rd, r * (int)ldo * 2 + cb);
+      ov[i] = bld16(ro, r * (int)ldo * 2 + cb);
     }
   };
   // own key block: K / V rows kb + kt2*16 + t, as B-operand fragments
@@ -491,14 +517,15 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   bf16x8 kf[2][2], vf[2][2];
   auto load_kv = [&](int it_) {
     const int tv = lane_tid() & 63;
-    const bf16_t* kb_ = qkv + (long)(it_ / H) * L * ldq + (it_ % H) * 64 + D + (tv >> 4) * 8;
+    const auto rq = rows_rsrc(qkv, (long)(it_ / H) * L, ldq * 2, it_ < n_items);
+    const int cb = ((it_ % H) * 64 + D + (tv >> 4) * 8) * 2;
 #pragma unroll
     for (int kt2 = 0; kt2 < 2; ++kt2) {
       const int key = kb + kt2 * 16 + (tv & 15);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16_t* src = kb_ + key * (int)ldq + s * 32;
-        uint4 ku = ld16_or_zero(src, key < L), vu = ld16_or_zero(src + D, key < L);
+        const int off = key * (int)ldq * 2 + cb + s * 64;
+        uint4 ku = bld16(rq, off), vu = bld16(rq, off + D * 2);
         kf[kt2][s] = *reinterpret_cast<bf16x8*>(&ku);
         vf[kt2][s] = *reinterpret_cast<bf16x8*>(&vu);
       }
@@ -510,6 +537,26 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
 
   // one row's 64 head columns (lane g holds columns dt*16 + 4g + {0..3} in x[dt], the 4 lanes
   // t, t+16, t+32, t+48 share the row) times mul, to dqkv columns col0..col0+63
+  // bf16 rows through the sequence's descriptor (row r of the sequence starting at row0; rows
+  // >= L dropped by the range check): store_row64's two 16-B pieces per lane
+  auto put_row_b = [&](long row0, int r, int col0, f32x4 x0, f32x4 x1, f32x4 x2, f32x4 x3,
+                       float mul) {
+    const f32x4 x[4] = {x0, x1, x2, x3};
+    const auto rs = rows_rsrc(dqkv, row0, lddq * 2, row0 >= 0);
+    uint2 xp[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      xp[dt] = uint2{pack2bf(x[dt][0] * mul, x[dt][1] * mul), pack2bf(x[dt][2] * mul, x[dt][3] * mul)};
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const auto s0 = __builtin_amdgcn_permlane16_swap(xp[2 * p].x, xp[2 * p + 1].x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(xp[2 * p].y, xp[2 * p + 1].y, false, false);
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const v4u v = v4u{s0[0], s1[0], s0[1], s1[1]};
+      __builtin_amdgcn_raw_buffer_store_b128(
+          v, rs, r * (int)lddq * 2 + (col0 + 32 * p + 16 * (g & 1) + 8 * (g >> 1)) * 2, 0, 0);
+    }
+  };
   auto put_row = [&](long row, int col0, f32x4 x0, f32x4 x1, f32x4 x2, f32x4 x3, float mul) {
     const f32x4 x[4] = {x0, x1, x2, x3};
     if constexpr (!Q8) {
@@ -541,14 +588,35 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
       }
     }
   };
+  // Persistent: item i's dQ rows are stored after item i+1's first barrier, not at the end of
+  // item i. CDNA's vmcnt retires loads and stores in issue order, so the wait for the prefetched
+  // rows at the top of item i+1 (hipcc emits vmcnt(0) there) would otherwise also wait for the
+  // dQ stores issued just before it — their whole latency exposed once per item.
+  f32x4 dQp[4][2];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dQp[dt][0] = dQp[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  long pbase = -1;
+  int ph = 0;
+  auto put_dq = [&](long pb, int hh, const f32x4 (&x)[4][2]) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int q = 32 * w + qt * 16 + t;
+      if constexpr (!Q8)
+        put_row_b(pb, q, hh * 64, x[0][qt], x[1][qt], x[2][qt], x[3][qt], scale);
+      else if (pb >= 0 && q < L)
+        put_row(pb + q, hh * 64, x[0][qt], x[1][qt], x[2][qt], x[3][qt], scale);
+    }
+  };
 #pragma unroll 1
   for (; item < n_items; item += gridDim.x) {
   const int next = item + gridDim.x;
   const int h = item % H;
   const long base = (long)(item / H) * L;
+  const int tvh = lane_tid();  // LDS addresses recomputed per item (hoisted, they spilled)
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int r = (tid + i * NTH) >> 3;
+    const int r = (tvh + i * NTH) >> 3;
+    const int ch = tvh & 7;
     *reinterpret_cast<uint4*>(Qs + r * 128 + swz(r, ch) * 16) = qv[i];
     *reinterpret_cast<uint4*>(dOs + r * 128 + swz(r, ch) * 16) = dv[i];
     const uint32_t aa[4] = {ov[i].x, ov[i].y, ov[i].z, ov[i].w};
@@ -562,11 +630,14 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
     dsum += __shfl_xor(dsum, 4);
     if (ch == 0) {
       nd_s[r] = -dsum;
-      nlse_s[r] = -lv[i];
+      nlse_s[r] = r < L ? -lv[i] : -1e30f;
     }
   }
   __syncthreads();
-  if (PERSIST && next < n_items) load_rows(next);  // in flight through phases 1 and 2
+  if constexpr (PERSIST) {
+    put_dq(pbase, ph, dQp);  // the previous item's dQ (see above; none before the first item)
+    load_rows(next);         // in flight through phases 1 and 2 (zeros past the last item)
+  }
 
   const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
   const int tr0 = tr_off(t, g, 0), tr1 = tr_off(t, g, 1), tr2 = tr_off(t, g, 2), tr3 = tr_off(t, g, 3);
@@ -642,7 +713,10 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
 #pragma unroll
   for (int k2 = 0; k2 < 2; ++k2) {
     const int key = kb + k2 * 16 + t;
-    if (key < L) {  // every lane of the row (same t) takes this branch together
+    if constexpr (!Q8) {
+      put_row_b(base, key, D + h * 64, dK[0][k2], dK[1][k2], dK[2][k2], dK[3][k2], scale);
+      put_row_b(base, key, 2 * D + h * 64, dV[0][k2], dV[1][k2], dV[2][k2], dV[3][k2], 1.0f);
+    } else if (key < L) {  // every lane of the row (same t) takes this branch together
       put_row(base + key, D + h * 64, dK[0][k2], dK[1][k2], dK[2][k2], dK[3][k2], scale);
       put_row(base + key, 2 * D + h * 64, dV[0][k2], dV[1][k2], dV[2][k2], dV[3][k2], 1.0f);
     }
@@ -656,7 +730,7 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
       const int key = kb + kt2 * 16 + t;
       *reinterpret_cast<bf16x8*>(Ks + key * 128 + swz(key, s * 4 + g) * 16) = kf[kt2][s];
     }
-  if (PERSIST && next < n_items) {  // kf / vf, phase-1 accumulators dead until the next item
+  if constexpr (PERSIST) {  // kf / vf, phase-1 accumulators dead until the next item
     load_o(next);
     load_kv(next);
   }
@@ -691,14 +765,17 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
       dQ[dt][1] = mfma16(ka, bq1, dQ[dt][1]);
     }
   }
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int q = qb + qt * 16 + t;
-    if (q < L) put_row(base + q, h * 64, dQ[0][qt], dQ[1][qt], dQ[2][qt], dQ[3][qt], scale);
+  if constexpr (!PERSIST) {  // one item per workgroup (short sequences: many workgroups)
+    put_dq(base, h, dQ);
+    break;
   }
-  if constexpr (!PERSIST) break;  // one item per workgroup (short sequences: many workgroups)
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dQp[dt][0] = dQ[dt][0], dQp[dt][1] = dQ[dt][1];
+  pbase = base;
+  ph = h;
   __syncthreads();  // phase 2 done with Ks / dS^T before the next item's LDS image
   }
+  if (PERSIST && pbase >= 0) put_dq(pbase, ph, dQp);
 }
 
 // ------------------------------------------------------------------ backward, query-major (dQ)

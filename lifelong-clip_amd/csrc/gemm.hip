@@ -181,25 +181,46 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       }
     }
   };
-  // one lane's CPL outputs of row m: a single 8-B / 16-B bf16 store, or NQ 16-B f32 stores
-  auto store_bf = [&](void* base, long ld, long m, const float (&w)[CPL]) {
-    bf16_t* p = (bf16_t*)base + m * ld + n;
-    if constexpr (CPL == 8)  // nontemporal: the consumer is the next kernel (st_nt16)
-      st_nt16(p, pack2bf(w[0], w[1]), pack2bf(w[2], w[3]), pack2bf(w[4], w[5]), pack2bf(w[6], w[7]));
-    else
-      *reinterpret_cast<uint2*>(p) = uint2{pack2bf(w[0], w[1]), pack2bf(w[2], w[3])};
+  // one lane's CPL outputs of row m: a single 8-B / 16-B bf16 store, or NQ 16-B f32 stores,
+  // through a descriptor over this tile's rows < M (rows past M dropped by the range check: no
+  // row-guard branch, so hipcc keeps the stores in flight instead of draining them with
+  // vmcnt(0) at every row group — 16 store-latency waits per 256x256 tile before)
+  const int rows_here = (M - m0) < BM ? (M - m0) : BM;
+  auto tile_rsrc = [&](void* base, long ld, int esize) {
+    return lc_rsrc(static_cast<char*>(base) + (long)m0 * ld * esize, (long)rows_here * ld * esize);
   };
-  auto store_f = [&](void* base, long ld, long m, const float (&w)[CPL]) {
-    float* p = (float*)base + m * ld + n;
+  auto store_bf = [&](const __amdgpu_buffer_rsrc_t& rs, long ld, long m, const float (&w)[CPL]) {
+    const int off = (int)(((m - m0) * ld + n) * 2);
+    if constexpr (CPL == 8)  // nontemporal (aux 2): the consumer is the next kernel
+      __builtin_amdgcn_raw_buffer_store_b128(
+          lc_u32x4{pack2bf(w[0], w[1]), pack2bf(w[2], w[3]), pack2bf(w[4], w[5]), pack2bf(w[6], w[7])},
+          rs, off, 0, 2);
+    else
+      __builtin_amdgcn_raw_buffer_store_b64(lc_u32x2{pack2bf(w[0], w[1]), pack2bf(w[2], w[3])}, rs,
+                                            off, 0, 0);
+  };
+  auto store_f = [&](const __amdgpu_buffer_rsrc_t& rs, long ld, long m, const float (&w)[CPL]) {
+    const int off = (int)(((m - m0) * ld + n) * 4);
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
-      *reinterpret_cast<float4*>(p + 4 * q) = make_float4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(lc_u32x4, f32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]}),
+          rs, off + 16 * q, 0, 0);
   };
+  constexpr bool OUT0_F = (EPI == EPI_F32 || EPI == EPI_RESID || EPI == EPI_AD_UP);
+  constexpr bool HAS_OUT1 = (EPI == EPI_GELU || EPI == EPI_BF16_F32 || EPI == EPI_GELU_D);
+  constexpr bool Q8OUT = (EPI == EPI_GELU_D_Q8 || EPI == EPI_MUL_Q8);
+  // (descriptors of absent outputs are built from their null pointer and never used; the fp8
+  // outputs' ldo1 is in bytes)
+  const __amdgpu_buffer_rsrc_t rs0 = tile_rsrc(EPI != EPI_MUL_Q8 ? out0 : nullptr, ldo0, OUT0_F ? 4 : 2);
+  const __amdgpu_buffer_rsrc_t rs1 = tile_rsrc(HAS_OUT1 || Q8OUT ? out1 : nullptr,
+                                               HAS_OUT1 || Q8OUT ? ldo1 : 0,
+                                               EPI == EPI_BF16_F32 ? 4 : (Q8OUT ? 1 : 2));
   // one lane's 8 outputs of row m as e4m3 in the fp8 operand format: the 4 lanes of a 32-column
   // block (consecutive, 4-aligned: LPR is a multiple of 4) share one E8M0 scale; the arithmetic
-  // is quant_fp8_kernel's on the bf16-rounded values. All 4 lanes of a block hold the same row,
-  // so they skip (m >= M) together and the shuffles stay inside active lanes.
-  auto store_q8 = [&](void* base, long ld, long m, const float (&w)[CPL]) {
+  // is quant_fp8_kernel's on the bf16-rounded values. All 4 lanes of a block hold the same row
+  // (every lane is active: rows >= M are dropped by the descriptor, not skipped).
+  auto store_q8 = [&](void*, long ld, long m, const float (&w)[CPL]) {
     if constexpr (CPL == 8) {  // every fp8-output epilogue (no f32 output)
       float q[8];
       uint32_t amax = 0;
@@ -212,10 +233,14 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       amax = max(amax, (uint32_t)__shfl_xor((int)amax, 2));
       const uint32_t byte = e8m0_of_bits(amax);
       const float inv = e8m0_inv(byte);
-      *reinterpret_cast<uint2*>((uint8_t*)base + m * ld + n) =
-          uint2{pack4_fp8(q[0] * inv, q[1] * inv, q[2] * inv, q[3] * inv),
-                pack4_fp8(q[4] * inv, q[5] * inv, q[6] * inv, q[7] * inv)};
-      if ((lane & 3) == 0) ep.q_scale[fp8_scale_index(m, n >> 5, ep.q_rows)] = (uint8_t)byte;
+      // codes through the tile descriptor (rows >= M dropped); the scale byte from all 4 lanes
+      // of the block (the same value to the same address; rows up to the tile end stay inside
+      // the 256-row-padded scale array) — no branch, like the bf16 stores
+      __builtin_amdgcn_raw_buffer_store_b64(
+          lc_u32x2{pack4_fp8(q[0] * inv, q[1] * inv, q[2] * inv, q[3] * inv),
+                   pack4_fp8(q[4] * inv, q[5] * inv, q[6] * inv, q[7] * inv)},
+          rs1, (int)((m - m0) * ld + n), 0, 0);
+      ep.q_scale[fp8_scale_index(m, n >> 5, ep.q_rows)] = (uint8_t)byte;
     }
   };
   // bf16 element i of a lane's packed side input
@@ -250,26 +275,25 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
 #if defined(G8_NOSTORE) && G8_NOSTORE == 2  // diagnostic builds only: global stores off
       if (ep.dbg == nullptr) continue;
 #endif
-      if (m >= M) continue;
       float w[CPL];
       if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_F32) {
-        store_bf(out0, ldo0, m, v);
-        if constexpr (EPI == EPI_BF16_F32) store_f(out1, ldo1, m, v);
+        store_bf(rs0, ldo0, m, v);
+        if constexpr (EPI == EPI_BF16_F32) store_f(rs1, ldo1, m, v);
       } else if constexpr (EPI == EPI_F32) {
-        store_f(out0, ldo0, m, v);
+        store_f(rs0, ldo0, m, v);
       } else if constexpr (EPI == EPI_RESID) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = xf[i] + v[i];
-        store_f(out0, ldo0, m, w);
+        store_f(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_GELU) {
-        store_bf(out0, ldo0, m, v);
+        store_bf(rs0, ldo0, m, v);
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = quick_gelu(v[i]);
-        store_bf(out1, ldo1, m, w);
+        store_bf(rs1, ldo1, m, w);
       } else if constexpr (EPI == EPI_GELU_BWD) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = v[i] * quick_gelu_grad(bfv(xb, i));
-        store_bf(out0, ldo0, m, w);
+        store_bf(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_GELU_D || EPI == EPI_GELU_D_Q8) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) {
@@ -277,35 +301,35 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
           w[i] = v[i] * sg;                                            // QuickGELU
           v[i] = sg * __builtin_fmaf(1.702f * v[i], 1.0f - sg, 1.0f);  // QuickGELU'
         }
-        store_bf(out0, ldo0, m, v);
+        store_bf(rs0, ldo0, m, v);
         if constexpr (EPI == EPI_GELU_D_Q8)
           store_q8(out1, ldo1, m, w);
         else
-          store_bf(out1, ldo1, m, w);
+          store_bf(rs1, ldo1, m, w);
       } else if constexpr (EPI == EPI_MUL || EPI == EPI_MUL_Q8) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = v[i] * bfv(xb, i);
         if constexpr (EPI == EPI_MUL_Q8)
           store_q8(out1, ldo1, m, w);
         else
-          store_bf(out0, ldo0, m, w);
+          store_bf(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_DOWN) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = fmaxf(v[i], 0.f) * drop_mul(seed, m, n + i, ep.keep);
-        store_bf(out0, ldo0, m, w);
+        store_bf(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_UP) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = xf[i] + bfv(xb, i) + ep.scale * v[i];
-        store_f(out0, ldo0, m, w);
+        store_f(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_MASK) {
         const float inv = 1.0f / ep.keep;
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = bfv(xb, i) > 0.f ? v[i] * inv : 0.f;
-        store_bf(out0, ldo0, m, w);
+        store_bf(rs0, ldo0, m, w);
       } else if constexpr (EPI == EPI_AD_ADD) {
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = bfv(xb, i) + v[i];
-        store_bf(out0, ldo0, m, w);
+        store_bf(rs0, ldo0, m, w);
       }
     }
   }

@@ -195,6 +195,20 @@ LC_DEV bf16x8 tr_frag(const char* lds, int row, int col) {
 // a global_load_lds target and in front of __syncthreads() — draining the ring every step. The
 // forms below are inline asm: the caller owns the waits (lds_wait0 before the first use of a
 // result, counted vmcnt waits before the barrier that publishes a slot).
+// Wave-uniform raw-buffer descriptor over `bytes` bytes at p (stride 0). Accesses at offsets
+// outside [0, bytes) are dropped (stores) or read 0 (loads) by the hardware range check, so a
+// row guard needs no branch: hipcc's vmcnt bookkeeping stays exact across such accesses (a
+// store under a branch makes it wait vmcnt(0) at the next use of an earlier load).
+LC_DEV __amdgpu_buffer_rsrc_t lc_rsrc(const void* p, long bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+typedef unsigned int lc_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int lc_u32x2 __attribute__((ext_vector_type(2)));
+
 LC_DEV uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }
