@@ -61,11 +61,12 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
 
 def routes_to_pp(M, N, K, epi):
     """The lc_gemm_nt tile selector's rule for the 256x256 phase-interleaved kernel (gemm.hip,
-    lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step. The c_proj dX x
-    QuickGELU' GEMM (EPI_MUL, K <= 1024, N >= 2048) goes to the 4-wave kernel instead."""
+    lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step. LC_GEMM_MUL_W4=1 sends the
+    c_proj dX x QuickGELU' GEMM (EPI_MUL, K <= 1024, N >= 2048) to the 4-wave kernel instead."""
     g8 = N % 128 == 0 and M >= 4096 and N % 256 == 0 and (M + 255) // 256 * (N // 256) >= 256
     from lcclip.ops import EPI_MUL
-    return g8 and not (epi == EPI_MUL and K <= 1024 and N >= 2048)
+    w4 = os.environ.get("LC_GEMM_MUL_W4", "") == "1"
+    return g8 and not (w4 and epi == EPI_MUL and K <= 1024 and N >= 2048)
 
 
 class GemmTimer:
@@ -385,9 +386,9 @@ def main():
                                     "mfma_frac_step_bound = the same with the whole step time "
                                     "(a lower bound of mfma_frac)"},
             "roofline": {"bound": "mfma",
-                         "kernel": "gemm8_kernel<EPI 0|2|6, bf16> (256x256 phase-interleaved "
+                         "kernel": "gemm8_kernel<EPI 0|2|6|7, bf16> (256x256 phase-interleaved "
                                    "bf16 MFMA GEMM: QKV, out-proj, c_fc+QuickGELU+QuickGELU', "
-                                   "c_proj fwd; QKV, out-proj, c_fc dX)",
+                                   "c_proj fwd; QKV, out-proj, c_fc, c_proj dX)",
                          "achieved": round(achieved / 1e12, 2), "peak": PEAK_BF16 / 1e12,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16, 4),
                          "traffic": None if traffic is None else round(traffic),

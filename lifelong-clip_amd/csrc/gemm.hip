@@ -1840,11 +1840,13 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     else if (M >= 4096 && N % 256 == 0 && 2 * t256 >= cus && K >= 2048) tile = 8;
     else if (M >= 4096 && N <= 768) tile = 4;
     else tile = 1;
-    // c_proj dX x QuickGELU' (N 3072, K 768): the 4-wave kernel, 289 vs 295 us (bench_gemm.py)
-    // (LC_GEMM_MUL_W4=0 keeps it on gemm8: in-step A/Bs)
+    // c_proj dX x QuickGELU' (N 3072, K 768): gemm8 since its epilogue stores went branch-free
+    // (260 vs 267-271 us for the 4-wave kernel standalone, step +0.4 %, profiles/r03/s2/
+    // r_ab_mul_route.txt; before that the 4-wave kernel won, 289 vs 295 us). LC_GEMM_MUL_W4=1
+    // routes it to the 4-wave kernel again (A/Bs).
     static const bool mul_w4 = [] {
       const char* e = getenv("LC_GEMM_MUL_W4");
-      return !(e && e[0] == '0');
+      return e && e[0] == '1';
     }();
     if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048 && mul_w4) tile = 7;
     // one-k-tile streams (adapter up-projection / input gradient, K = 64): 128x64 tiles keep
