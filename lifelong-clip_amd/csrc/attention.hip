@@ -101,7 +101,9 @@ LC_DEV void store_row64(bf16_t* row, int g, const uint2 (&x)[4]) {
 constexpr int V_STRIDE = 160;  // bytes per V row in the forward's plain V image (conflict-free tr)
 
 // ----------------------------------------------------------------------------------- forward
-template <int NQB>
+// ONLINE: one pass over the keys with a running row max (the O accumulators and row sums
+// rescaled when it grows) instead of the exact two-pass form (LCCLIP_ATTN_FWD_ONLINE=1, A/Bs)
+template <int NQB, bool ONLINE = false>
 __global__ void __launch_bounds__(64 * NQB, 4)
 attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
                 bf16_t* __restrict__ O, long ldo, float* __restrict__ lse, int causal,
@@ -181,7 +183,7 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   // pass 1: exact row max of the raw scores
   float mx[2] = {-INFINITY, -INFINITY};
 #pragma unroll 1
-  for (int s = 0; s < s_end; ++s) {
+  for (int s = 0; s < (ONLINE ? 0 : s_end); ++s) {
     f32x4 S[2][2];
     scores(s, S);
 #pragma unroll
@@ -208,10 +210,27 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   f32x4 Oa[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) Oa[dt][0] = Oa[dt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mr[2] = {-INFINITY, -INFINITY};  // ONLINE: running raw-score max per query
 #pragma unroll 1
   for (int s = 0; s < s_end; ++s) {
     f32x4 S[2][2];
     scores(s, S);
+    if constexpr (ONLINE) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        float m = fmaxf(fmaxf(fmaxf(S[0][qt][0], S[0][qt][1]), fmaxf(S[0][qt][2], S[0][qt][3])),
+                        fmaxf(fmaxf(S[1][qt][0], S[1][qt][1]), fmaxf(S[1][qt][2], S[1][qt][3])));
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const float mn = fmaxf(mr[qt], m);  // finite from block 0 on (key 0 is never masked)
+        const float corr = ex2((mr[qt] - mn) * c);
+        mr[qt] = mn;
+        nm[qt] = -mn * c;
+        sm[qt] *= corr;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) Oa[dt][qt] *= corr;
+      }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -232,6 +251,7 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
       Oa[dt][1] = mfma16(vf, pb1, Oa[dt][1]);
     }
   }
+  if constexpr (ONLINE) mx[0] = mr[0] * c, mx[1] = mr[1] * c;
   // lane holds O^T[d = dt*16 + 4g + r][q = qb + qt*16 + t]
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
@@ -938,11 +958,19 @@ int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
   const int nqb = (L + 31) / 32;
   dim3 grid(n_seq * H);
   const float scale = 0.125f;  // 64^-0.5
+  static const bool online = [] {
+    const char* e = getenv("LCCLIP_ATTN_FWD_ONLINE");
+    return e && e[0] == '1';
+  }();
   switch (nqb) {
 #define LC_AF(Q)                                                                                \
   case Q:                                                                                      \
-    hipLaunchKernelGGL(attn_fwd_kernel<Q>, grid, dim3(64 * Q), 0, st, L, H, D,                 \
-                       (const bf16_t*)qkv, ldq, (bf16_t*)O, ldo, lse, causal, scale);          \
+    if (online)                                                                                \
+      hipLaunchKernelGGL((attn_fwd_kernel<Q, true>), grid, dim3(64 * Q), 0, st, L, H, D,       \
+                         (const bf16_t*)qkv, ldq, (bf16_t*)O, ldo, lse, causal, scale);        \
+    else                                                                                       \
+      hipLaunchKernelGGL((attn_fwd_kernel<Q, false>), grid, dim3(64 * Q), 0, st, L, H, D,      \
+                         (const bf16_t*)qkv, ldq, (bf16_t*)O, ldo, lse, causal, scale);        \
     break;
     LC_AF(1) LC_AF(2) LC_AF(3) LC_AF(4) LC_AF(5) LC_AF(6) LC_AF(7) LC_AF(8)
 #undef LC_AF
