@@ -101,9 +101,12 @@ LC_DEV void store_row64(bf16_t* row, int g, const uint2 (&x)[4]) {
 constexpr int V_STRIDE = 160;  // bytes per V row in the forward's plain V image (conflict-free tr)
 
 // ----------------------------------------------------------------------------------- forward
-// ONLINE: one pass over the keys with a running row max (the O accumulators and row sums
-// rescaled when it grows) instead of the exact two-pass form (LCCLIP_ATTN_FWD_ONLINE=1, A/Bs)
-template <int NQB, bool ONLINE = false>
+// ONLINE (default): one pass over the keys with a running row max — the O accumulators and row
+// sums rescaled by exp2((m_old - m_new) c) per 32-key block — instead of the exact two-pass form
+// (a first pass of S = K Q^T for the max alone): a third fewer MFMAs and K reads, image forward
+// 103.4 -> 94.8 us standalone (profiles/r03/s2/u_ab_attn_online.txt). LCCLIP_ATTN_FWD_ONLINE=0
+// selects the two-pass form (A/Bs).
+template <int NQB, bool ONLINE = true>
 __global__ void __launch_bounds__(64 * NQB, 4)
 attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
                 bf16_t* __restrict__ O, long ldo, float* __restrict__ lse, int causal,
@@ -960,7 +963,7 @@ int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
   const float scale = 0.125f;  // 64^-0.5
   static const bool online = [] {
     const char* e = getenv("LCCLIP_ATTN_FWD_ONLINE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   switch (nqb) {
 #define LC_AF(Q)                                                                                \

@@ -190,28 +190,6 @@ class OnlineTrainer:
         else:
             self._txt_cache.clear()
 
-    @staticmethod
-    def _new_side_stream(dev):
-        """A side HIP stream; LCCLIP_SIDE_CU_STRIDE=k (A/B experiments) restricts it to every k-th
-        CU (hipExtStreamCreateWithCUMask), so side-stream kernels cannot displace main-chain
-        GEMM tiles on the other CUs."""
-        k = int(os.environ.get("LCCLIP_SIDE_CU_STRIDE", "0") or 0)
-        if k <= 1:
-            return torch.cuda.Stream(device=dev)
-        import ctypes
-        hip = ctypes.CDLL("libamdhip64.so")
-        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-        words = (n_cu + 31) // 32
-        mask = (ctypes.c_uint32 * words)()
-        for cu in range(0, n_cu, k):
-            mask[cu // 32] |= 1 << (cu % 32)
-        handle = ctypes.c_void_p()
-        with torch.cuda.device(dev):
-            rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(words), mask)
-        if rc != 0:
-            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-        return torch.cuda.ExternalStream(handle.value, device=dev)
-
     def _grad_stream(self, dev):
         if not self.overlap_grads:
             return None
@@ -220,7 +198,7 @@ class OnlineTrainer:
             if side is not None:
                 return side
         if self._gstream is None:
-            self._gstream = self._new_side_stream(dev)
+            self._gstream = torch.cuda.Stream(device=dev)
         return self._gstream
 
     def _merge_side_streams(self):
@@ -243,7 +221,7 @@ class OnlineTrainer:
         if not self.overlap_text:
             return None
         if self._side is None:
-            self._side = self._new_side_stream(dev)
+            self._side = torch.cuda.Stream(device=dev)
         return self._side
 
     def _img_bucket_hook(self):
