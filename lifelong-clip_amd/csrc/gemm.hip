@@ -714,10 +714,6 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   const int wr = wave / WN, wc = wave % WN;
   const int tiles_n = N / BN;
   int bid = blockIdx.x;
-  // diagnostic: offset every other first-round workgroup of each XCD by ep.stagger x ~3.4 us so
-  // the CUs' epilogue store bursts stop coinciding (LC_GEMM_STAGGER; 0 in production)
-  if (ep.stagger > 0 && bid < 256 && ((bid >> 3) & 1))
-    for (int i = 0; i < ep.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   int split = -1;
   int tb = 0, te = K / KT;  // k-tiles [tb, te) of this workgroup
   if (bid < sk.dp_tiles) {
@@ -1759,11 +1755,6 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
               long ws_bytes, const Fp8Scales& sc) {
   EpiParams ep = ep_in;
   ep.group_m = group_m(N);
-  static const int stagger = [] {
-    const char* e = getenv("LC_GEMM_STAGGER");
-    return e ? atoi(e) : 0;
-  }();
-  ep.stagger = stagger;
   const int tiles = ((M + 255) / 256) * (N / 256);
   const int units = K / (FP8 ? 128 : 64);
   // (LC_GEMM_SPLIT_MIN overrides the minimum k-tiles per split-K slice: in-step A/Bs)

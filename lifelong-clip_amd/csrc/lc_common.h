@@ -117,7 +117,6 @@ struct EpiParams {
   uint8_t* q_scale;  // fp8-output epilogues: E8M0 scales of the fp8 output ([N/128][q_rows][4])
   long q_rows;       // padded row count of that scale buffer
   int group_m;       // 256x256 GEMMs: tile raster groups of group_m row panels (0/1: row-major)
-  int stagger;       // diagnostic (LC_GEMM_STAGGER): first-round delay of every other workgroup
 };
 
 // fp8 operand scales of a block-scaled GEMM (see fp8_scale_index)
