@@ -18,5 +18,5 @@ python tools/trace_by_shape.py $P/trace/run_kernel_trace.csv 8 45 > gpurun_out/r
 P=gpurun_out/prof_adapter
 run trace_adapter 300 rocprofv3 --kernel-trace --stats --output-format csv -d $P/trace -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline
 python tools/trace_by_shape.py $P/trace/run_kernel_trace.csv 8 45 > gpurun_out/r03_adapter_by_shape.txt 2>&1
-bash tools/gpu_r3_maple.sh
+bash tools/ab/gpu_r3_maple.sh
 echo done
