@@ -148,6 +148,17 @@ int lc_layernorm_bwd(hipStream_t stream, int rows, int D, const void* dy, int dy
                      const float* gamma, const float* dres, float* dx, void* dx_bf16, long ldo,
                      const int* row_idx);
 
+/* lc_layernorm_bwd (no row gather) whose result is also written as the next fp8 GEMM's A
+ * operand: e4m3 codes q [rows, ldq bytes] + E8M0 scales (q_scale, q_rows as in
+ * lc_layernorm_fwd_fp8), bit-identical to dx_bf16 followed by lc_quant_fp8. Used by the fp8
+ * towers for the block output gradient the next (lower) block's c_proj input-gradient GEMM
+ * quantises. Replaces: autograd of F.layer_norm (model.py:199) under MaPLe's fp8 mode. */
+int lc_layernorm_bwd_fp8(hipStream_t stream, int rows, int D, const void* dy, int dy_f32,
+                         long ldy, const float* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, float* dx, void* dx_bf16,
+                         long ldo, const int* row_idx, void* q, long ldq, void* q_scale,
+                         long q_rows);
+
 /* im2col of NCHW f32 images into bf16 patches [n*g*g, 3*P*P] in conv1's (c, kh, kw) order.
  * Replaces: the input side of conv1 (model.py:756-758). */
 int lc_patchify(hipStream_t stream, int n_img, int res, int patch, const float* img, void* out);

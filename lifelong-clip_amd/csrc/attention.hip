@@ -478,7 +478,6 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
   // staging: 16-B chunks of Q, dO and O rows (8 lanes per row); D = rowsum(dO*O) from the same
   // chunks (xor-shuffles) when they are written to LDS
   constexpr int IT = LP * 8 / NTH;  // = 4
-  const int ch = tid & 7;
   uint4 qv[IT], dv[IT], ov[IT];
   float lv[IT];
   // Every global access of an item goes through a raw-buffer descriptor over that sequence's L

@@ -142,7 +142,8 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
               const float* __restrict__ x, long ldx, const float* __restrict__ mean,
               const float* __restrict__ rstd, const float* __restrict__ gamma,
               const float* __restrict__ dres, float* __restrict__ dx, bf16_t* __restrict__ dxb,
-              long ldo, const int* __restrict__ row_idx) {
+              long ldo, const int* __restrict__ row_idx, uint8_t* __restrict__ qo, long ldq,
+              uint8_t* __restrict__ q_scale, long q_rows) {
   constexpr int D = V * 64;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -185,6 +186,9 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   }
   store_row_f32<V>(dx + xr * ldo, lane, out);
   if (dxb) store_row_bf16<V>(dxb + xr * ldo, lane, out);
+  // the bf16 result also as the next fp8 GEMM's operand (the codes of dxb + quant_fp8)
+  if constexpr (V % 4 == 0)
+    if (qo) store_row_fp8<V>(qo + xr * ldq, q_scale, q_rows, xr, lane, out);
 }
 
 // im2col for conv1 (k = s = P): out[(n*g*g + py*g + px)][c*P*P + ky*P + kx] = img[n][c][py*P+ky][px*P+kx]
@@ -266,6 +270,27 @@ int grid_for(long work, int block) {
   return (int)(g < 1 ? 1 : g);
 }
 
+int ln_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy, const float* x,
+           long ldx, const float* mean, const float* rstd, const float* gamma, const float* dres,
+           float* dx, void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
+           void* q_scale, long q_rows) {
+  LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
+  if (rows == 0) return LC_OK;
+  dim3 grid((rows + 3) / 4), block(256);
+  switch (D / 64) {
+#define LC_LN_B(V)                                                                              \
+  case V:                                                                                      \
+    hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy, x, ldx,    \
+                       mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16, ldo, row_idx,            \
+                       (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);                            \
+    break;
+    LC_LN_B(1) LC_LN_B(2) LC_LN_B(4) LC_LN_B(8) LC_LN_B(12) LC_LN_B(16)
+    default:
+      return LC_EINVAL;
+#undef LC_LN_B
+  }
+  LC_LAUNCH_RET();
+}
 }  // namespace
 
 extern "C" {
@@ -308,25 +333,25 @@ int lc_layernorm_fwd_fp8(hipStream_t st, int rows, int D, const float* x, long l
                 q_rows);
 }
 
+
 int lc_layernorm_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
                      const float* x, long ldx, const float* mean, const float* rstd,
                      const float* gamma, const float* dres, float* dx, void* dx_bf16, long ldo,
                      const int* row_idx) {
-  LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
-  if (rows == 0) return LC_OK;
-  dim3 grid((rows + 3) / 4), block(256);
-  switch (D / 64) {
-#define LC_LN_B(V)                                                                              \
-  case V:                                                                                      \
-    hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy, x, ldx,    \
-                       mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16, ldo, row_idx);           \
-    break;
-    LC_LN_B(1) LC_LN_B(2) LC_LN_B(4) LC_LN_B(8) LC_LN_B(12) LC_LN_B(16)
-    default:
-      return LC_EINVAL;
-#undef LC_LN_B
-  }
-  LC_LAUNCH_RET();
+  return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
+                row_idx, nullptr, 0, nullptr, 0);
+}
+
+int lc_layernorm_bwd_fp8(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
+                         const float* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, float* dx, void* dx_bf16,
+                         long ldo, const int* row_idx, void* q, long ldq, void* q_scale,
+                         long q_rows) {
+  LC_CHECK_ARG(D % 256 == 0 && q != nullptr && q_scale != nullptr && ldq >= D && ldq % 16 == 0 &&
+               ((uintptr_t)q & 15) == 0 && q_rows % 256 == 0 && row_idx == nullptr &&
+               q_rows >= (rows + 255) / 256 * 256);
+  return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
+                row_idx, q, ldq, q_scale, q_rows);
 }
 
 int lc_patchify(hipStream_t st, int n_img, int res, int patch, const float* img, void* out) {

@@ -34,6 +34,8 @@ SIGNATURES = {
     "lc_layernorm_fwd_fp8": [P, c_int, c_int, P, c_long, P, P, P, P, c_long, P, P, P, c_long, P,
                              c_long],
     "lc_layernorm_bwd": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long, P],
+    "lc_layernorm_bwd_fp8": [P, c_int, c_int, P, c_int, c_long, P, c_long, P, P, P, P, P, P, c_long,
+                             P, P, c_long, P, c_long],
     "lc_patchify": [P, c_int, c_int, c_int, P, P],
     "lc_vit_assemble": [P, c_int, c_int, c_int, P, P, P, P],
     "lc_text_embed": [P, c_int, c_int, c_int, P, P, P, P],

@@ -192,8 +192,9 @@ class BlockStack:
     # EPI_MUL_Q8), the ln_1 / ln_2 forwards and the attention backward write their result
     # straight in the fp8 operand format of the GEMM that consumes it instead of bf16 + a
     # quant_fp8 pass (the same codes). LCCLIP_FP8_FUSE for A/Bs: 0 none, 1 the GEMM epilogues,
-    # 2 + LayerNorm, 3 (default) + attention backward
-    FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "3"))
+    # 2 + LayerNorm, 3 + attention backward, 4 (default) + ln_1's backward (the block output
+    # gradient, no-adapter towers)
+    FUSE_Q8 = int(os.environ.get("LCCLIP_FP8_FUSE", "4"))
     # bf16 adapter towers: adapter + the following LayerNorm in one launch (LCCLIP_FUSE_LN=0: the
     # separate adapter_fwd + layernorm_fwd launches, for A/Bs)
     FUSE_LN = os.environ.get("LCCLIP_FUSE_LN", "1") != "0"
@@ -417,6 +418,12 @@ class BlockStack:
         # expand the current gradient into a free pair and compact their output back
         pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev))]
         cur = 0
+        # fp8 (no adapter: the block output gradient feeds c_proj dX directly): ln_1's backward
+        # also writes its result as the fp8 operand of the next (lower) block's c_proj dX GEMM
+        # (ops.layernorm_bwd_fp8), so that block skips quant_fp8. q_of[i]: the fp8 image of
+        # pairs[i]'s bf16 gradient while it is current (dropped when prompt rows change it).
+        fuse_ln_q = self._fused_q8(4) and self.variant != "adapter" and D % 256 == 0
+        q_mats, q_of = {}, {}
         for li in range(len(self.blocks) - 1, -1, -1):
             blk, st, s = self.blocks[li], self.staged[li], saved[li]
             if ev is not None:
@@ -428,6 +435,7 @@ class BlockStack:
                 if len(pairs) == 2:
                     pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev)))
                 e = 2 if cur != 2 else 1
+                q_of.clear()
                 for src, dst in zip(pairs[cur], pairs[e]):
                     v = dst[:Mx].view(n_seq, Lx, D)
                     v[:, :L] = src[:M].view(n_seq, L, D)
@@ -443,7 +451,9 @@ class BlockStack:
             else:
                 dY = gxb
             if q_da is not None:
-                q = ops.gemm_nt_fp8(ops.quant_fp8(dY), st.q["wprT"], EPI_MUL_Q8, None, aux=s["gd"],
+                qdy = q_of.pop(cur, None) if self.variant != "adapter" else None
+                qdy = qdy if qdy is not None and qdy.rows == Mx else ops.quant_fp8(dY)
+                q = ops.gemm_nt_fp8(qdy, st.q["wprT"], EPI_MUL_Q8, None, aux=s["gd"],
                                     q_out=q_da.narrow(Mx))
                 ops.gemm_nt_fp8(q, st.q["wfcT"], EPI_BF16, dh[:Mx])
             else:
@@ -483,8 +493,16 @@ class BlockStack:
                 ops.gemm_nt_fp8(qd, st.q["wqkvT"], EPI_BF16, dh[:Mx])
             else:
                 self._gemm(st, "wqkvT", dqkv[:Mx], EPI_BF16, dh[:Mx])
-            ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
-                              oxb, dres=dx_mid[:Mx])
+            if fuse_ln_q and "R" not in s and not P:
+                if out not in q_mats:
+                    q_mats[out] = ops.Fp8Mat(Mmax, D, dev)
+                q_of[out] = ops.layernorm_bwd_fp8(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"],
+                                                  blk.ln_1.weight, ox, oxb, q_mats[out].narrow(Mx),
+                                                  dres=dx_mid[:Mx])
+            else:
+                q_of.pop(out, None)
+                ops.layernorm_bwd(dh[:Mx], s["x_in"], s["mean1"], s["rstd1"], blk.ln_1.weight, ox,
+                                  oxb, dres=dx_mid[:Mx])
             ev = self._layer_done(li, grad_stream, on_layer)
             if "R" in s:
                 r0, pr = s["R"]

@@ -192,6 +192,19 @@ def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_id
     return dx
 
 
+def layernorm_bwd_fp8(dy, x, mean, rstd, weight, dx, dx_bf16, q, dres=None):
+    """layernorm_bwd whose result is also written into q, an Fp8Mat [rows, D]: the fp8 A operand
+    of the next GEMM (the codes of dx_bf16 + quant_fp8)."""
+    rows = dy.shape[0]
+    D = x.shape[1]
+    if q.rows != rows or q.K != D:
+        raise ValueError("layernorm_bwd_fp8: output shape mismatch")
+    call("lc_layernorm_bwd_fp8", stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+         dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
+         ptr(dx_bf16), dx.stride(0), None, ptr(q.data), q.data.stride(0), ptr(q.scales), q.rows_pad)
+    return q
+
+
 def patchify(img, patch, out):
     if img.dtype != F32 or not img.is_contiguous():
         raise ValueError("patchify expects a contiguous f32 NCHW batch")

@@ -180,6 +180,35 @@ def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D):
     assert torch.equal(y2, y) and torch.equal(m2, m1) and torch.equal(r2, r1)
 
 
+@pytest.mark.parametrize("rows,D", [(50432 // 16, 768), (301, 256), (1, 512)])
+def test_layernorm_bwd_fp8_matches_quant(ops, dev, rows, D):
+    """LayerNorm backward writing its result also as the fp8 operand of the next c_proj dX GEMM
+    (the fp8 towers' block output gradient) equals the bf16 LayerNorm backward followed by
+    quant_fp8 bit for bit, with identical f32 / bf16 outputs; with and without the residual
+    gradient, and a zero output-gradient row (all-zero blocks)."""
+    g = torch.Generator(device=dev).manual_seed(rows * 7 + D)
+    x = torch.randn(rows, D, device=dev, generator=g) * 2 + 0.5
+    w = torch.randn(D, device=dev, generator=g)
+    b = torch.randn(D, device=dev, generator=g)
+    y = torch.empty(rows, D, device=dev, dtype=BF)
+    mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+    ops.layernorm_fwd(x, w, b, y, mean, rstd)
+    dy = (torch.randn(rows, D, device=dev, generator=g) * 0.1).to(BF)
+    dy[0] = 0
+    for dres in (None, torch.randn(rows, D, device=dev, generator=g) * 0.01):
+        if dres is not None:
+            dres[0] = 0
+        dx1, dxb1 = torch.empty(rows, D, device=dev), torch.empty(rows, D, device=dev, dtype=BF)
+        ops.layernorm_bwd(dy, x, mean, rstd, w, dx1, dxb1, dres=dres)
+        ref = ops.quant_fp8(dxb1)
+        dx2, dxb2 = torch.empty_like(dx1), torch.empty_like(dxb1)
+        q = ops.layernorm_bwd_fp8(dy, x, mean, rstd, w, dx2, dxb2, ops.Fp8Mat(rows, D, dev),
+                                  dres=dres)
+        assert torch.equal(dx2, dx1) and torch.equal(dxb2, dxb1)
+        assert torch.equal(q.data, ref.data)
+        assert torch.equal(gpu_scales(q), gpu_scales(ref))
+
+
 @pytest.mark.parametrize("n_seq,L,H,causal", [(4, 197, 12, False), (2, 199, 12, False),
                                               (3, 77, 8, True), (2, 40, 2, False)])
 def test_attn_bwd_fp8_matches_quant(ops, dev, n_seq, L, H, causal):
