@@ -873,6 +873,25 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
 #else
   auto stamp = [](int) {};
 #endif
+#ifdef LC_GEMM_CLOCK
+  // in-kernel clock (tools/g8_clock.py, make CLOCK=1): shader-clock and 100 MHz stamps around
+  // the workgroup's tile, kept in SGPRs and written once at the end
+  const unsigned long long ck_t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long ck_r0 = __builtin_amdgcn_s_memrealtime();
+  auto clock_out = [&]() {
+    if (ep.dbg == nullptr) return;
+    __syncthreads();
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      unsigned long long* d = ep.dbg + 4L * blockIdx.x;
+      d[0] = t1 - ck_t0;
+      d[1] = r1 - ck_r0;
+      d[2] = ck_r0;
+      d[3] = r1;
+    }
+  };
+#endif
   stamp(0);
 
   // prologue: k-tile 0 whole, then B rows 0..255 of k-tile 1 (in flight across the barrier)
@@ -983,7 +1002,12 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     __syncthreads();
     const int last = flag[0];
     __syncthreads();
-    if (!last) return;
+    if (!last) {
+#ifdef LC_GEMM_CLOCK
+      clock_out();  // a slice that only wrote its slab
+#endif
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1006,6 +1030,9 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   __syncthreads();
   if (diag)
     for (int k = lane; k < TRACE_N; k += 64) ep.dbg[1 + wr * TRACE_N + k] = tr[k];
+#endif
+#ifdef LC_GEMM_CLOCK
+  clock_out();
 #endif
 }
 
