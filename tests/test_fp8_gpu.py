@@ -65,7 +65,7 @@ def test_quant_fp8_bitexact(ops, dev, rows, K, src):
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 256, 128), (4096 + 197, 768, 768), (1000, 2304, 3072),
-                                   (50432 // 4, 3072, 768)])
+                                   (50432 // 4, 3072, 768), (12800, 768, 3072)])
 def test_gemm_fp8_exact_integers(ops, dev, M, N, K):
     g = torch.Generator(device=dev).manual_seed(M + N + K)
     A = torch.randint(-8, 9, (M, K), device=dev, generator=g).float()

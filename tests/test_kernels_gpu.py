@@ -110,7 +110,8 @@ def test_gemm_nt_epilogues(ops, dev, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432, 3072, 768),
-                                   (296 * 256 - 100, 256, 2048), (50432, 768, 768)])
+                                   (296 * 256 - 100, 256, 2048), (50432, 768, 768),
+                                   (12800, 768, 3072), (12800 - 37, 768, 2304)])
 @pytest.mark.parametrize("tile", [0, 8])
 def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
     from lcclip import _lib
@@ -125,7 +126,8 @@ def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
 def _splitk_tail(ops, dev, M, N, K):
     """The split-K tail of the 256x256 ping-pong GEMM (lc_gemm_nt_ws): these shapes leave the
     last round over 256 CUs at most half full (591 / 2364 / 296 tiles), so their tail tiles are
-    summed from 3-4 K-slices. Small integers: every partial sum is exact in f32, so the result
+    summed from 3-4 K-slices; M = 12 800 (MaPLe's 64 images, 150 tiles: under one round) runs
+    whole tiles (splitting every tile was measured slower: profiles/r03/sk_ab). Small integers: every partial sum is exact in f32, so the result
     must equal torch's bit for bit, for both the split and the plain (ws = NULL) launch; the
     fused epilogue must see the summed tile exactly once (bias added once)."""
     from lcclip._lib import call, ptr, stream_of
