@@ -1,7 +1,7 @@
 // bf16 MFMA shape vs the clock the chip holds (dev tool; MI355X_MICROARCH.md 'DVFS give-back'
 // item 7, cdna_hip_programming.md §5.4 rule 28): the same register-resident MFMA stream on
 // v_mfma_f32_16x16x32_bf16 and v_mfma_f32_32x32x16_bf16, random operands rotated every MFMA, one
-// 256-thread workgroup per CU slot (4 waves, one per SIMD) x 2 per CU. After ~2 s of back-to-back
+// 256-thread workgroup per CU slot (4 waves, one per SIMD) x 1 or 2 per CU (argv[2]). After ~2 s of back-to-back
 // launches it reports TFLOP/s (HIP events), the in-kernel clock (s_memtime / s_memrealtime x
 // 100 MHz, median over workgroups) and the MFMA issue efficiency per clock.
 //   hipcc --offload-arch=gfx950 -O3 -o lifelong-clip_amd/lcclip/ab/mfma_shape_clock tools/mfma_shape_clock.hip
@@ -28,9 +28,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int NOP = 4;  // operand pairs rotated through
 
-// SHAPE 16: 8 independent 16x16x32 accumulators; SHAPE 32: 4 independent 32x32x16 ones (the
-// same 32 accumulator floats per lane per 4 MFMAs of work each way: 16x16x32 = 16 Kflop, 32x32x16
-// = 32 Kflop, so one 32x32 MFMA = two 16x16 ones).
+// SHAPE 16: 8 16x16x32 MFMAs per round on 4 accumulators; SHAPE 32: 4 32x32x16 ones on 4 (the
+// same work per round: 16x16x32 = 16 Kflop, 32x32x16 = 32 Kflop, one 32x32 MFMA = two 16x16).
 template <int SHAPE>
 __global__ void __launch_bounds__(256) mfma_loop(const bf16x8* __restrict__ src, float* __restrict__ dst,
                                                  int iters, unsigned long long* __restrict__ clk) {
@@ -45,19 +44,23 @@ __global__ void __launch_bounds__(256) mfma_loop(const bf16x8* __restrict__ src,
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   float s = 0.f;
   if constexpr (SHAPE == 16) {
-    f32x4 acc[8];
+    // 4 accumulators, each taking two MFMAs per round (8 per round as the 32x32 form's 4), issued
+    // in place by inline asm: through the builtin hipcc rotated them through AGPR copies (24
+    // v_accvgpr_* per 32 MFMAs)
+    f32x4 acc[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int it = 0; it < iters; it += NOP) {
 #pragma unroll
       for (int u = 0; u < NOP; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[(j + u) % NOP], b[(j + 3 * u) % NOP],
-                                                           acc[j], 0, 0, 0);
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                       : "+a"(acc[j & 3])
+                       : "v"(a[(j + u) % NOP]), "v"(b[(j + 3 * u) % NOP]));
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
+    for (int j = 0; j < 4; ++j) s += acc[j][0] + acc[j][1] + acc[j][2] + acc[j][3];
   } else {
     f32x16 acc[4];
 #pragma unroll
@@ -91,7 +94,8 @@ int main(int argc, char** argv) {
   const bool zero = argc > 1 && argv[1][0] == 'z';
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const int wgs = 2 * cus, iters = 4096;
+  const int per_cu = argc > 2 ? atoi(argv[2]) : 2;  // workgroups (= waves per SIMD) per CU
+  const int wgs = per_cu * cus, iters = 4096;
   const size_t nsrc = (size_t)wgs * 256 * 2 * NOP;
   std::vector<uint16_t> h(nsrc * 8);
   unsigned x = 12345;
@@ -110,7 +114,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  printf("data=%s wgs=%d (2 per CU, 4 waves each) iters=%d\n", zero ? "zeros" : "random", wgs, iters);
+  printf("data=%s wgs=%d (%d per CU, 4 waves each) iters=%d\n", zero ? "zeros" : "random", wgs, per_cu,
+         iters);
   for (int shape : {16, 32, 16, 32}) {
     auto launch = [&]() {
       if (shape == 16)
@@ -145,7 +150,7 @@ int main(int argc, char** argv) {
     const double flops = (double)wgs * 4 * iters * 4 * 32768.0;
     const double tf = flops / (ms * 1e-3) / 1e12;
     // per-clock: the dense bf16 rate is 2.5 PF at 2.4 GHz = 1024 flop / SIMD / clock
-    const double need = (double)iters * 4 * 32768.0 * 2 / 1024.0;  // cycles per SIMD (2 waves)
+    const double need = (double)iters * 4 * 32768.0 * per_cu / 1024.0;  // cycles per SIMD
     printf("shape %dx%d: %.3f ms  %.0f TF (%.3f of 2.5 PF)  clock %.3f GHz (median, min %.3f max %.3f)"
            "  issue eff %.3f  (TF / (clock x 1024 flop x 1024 SIMDs) %.3f)\n",
            shape, shape, ms, tf, tf / 2500.0, ghz[wgs / 2], ghz[0], ghz[wgs - 1], need / cyc,
