@@ -61,12 +61,8 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
 
 def routes_to_pp(M, N, K, epi):
     """The lc_gemm_nt tile selector's rule for the 256x256 phase-interleaved kernel (gemm.hip,
-    lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step. LC_GEMM_MUL_W4=1 sends the
-    c_proj dX x QuickGELU' GEMM (EPI_MUL, K <= 1024, N >= 2048) to the 4-wave kernel instead."""
-    g8 = N % 128 == 0 and M >= 4096 and N % 256 == 0 and (M + 255) // 256 * (N // 256) >= 256
-    from lcclip.ops import EPI_MUL
-    w4 = os.environ.get("LC_GEMM_MUL_W4", "") == "1"
-    return g8 and not (w4 and epi == EPI_MUL and K <= 1024 and N >= 2048)
+    lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step."""
+    return N % 128 == 0 and M >= 4096 and N % 256 == 0 and (M + 255) // 256 * (N // 256) >= 256
 
 
 class GemmTimer:

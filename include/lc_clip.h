@@ -96,7 +96,8 @@ int lc_quant_fp8(hipStream_t stream, long rows, int K, const void* src, int src_
  * 5 = 256x256 ping-pong (8 waves in two staggered groups, 4-slot k-half LDS ring), 6 = same,
  * 7 = 256x256 4-wave AGPR kernel, 8 = 256x256 phase-interleaved kernel (the fp8 GEMM's, bf16),
  * 11 = 128x64 one-stage.
- * The environment variable LC_GEMM_TILE sets the initial value. */
+ * (A diagnostic build, make DIAG=1, also takes the initial value from LC_GEMM_TILE; the
+ * production library reads no environment variables.) */
 int lc_gemm_set_tile(int tile);
 
 /* Diagnostic (builds with -DLC_GEMM_TRACE only): when p != NULL, the ping-pong GEMM stores
@@ -304,6 +305,10 @@ int lc_adapter_ln_fwd(hipStream_t stream, int M, int D, const void* z, long ldz,
 int lc_adapter_bwd(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
                    void* dz, long ldz);
+
+/* Testing: the form lc_adapter_bwd uses at D = 512 / 768 — 1 (default) the one-pass row-block
+ * kernel, 0 the two skinny GEMMs (EPI_AD_MASK + EPI_AD_ADD) it must equal bit for bit. */
+int lc_adapter_bwd_set_form(int fused);
 
 /* Adapter weight and bias gradients of one application, accumulated (f32, one launch):
  *   dWu [D,64] += scale * gout^T h      dbu [D]  += scale * sum_m gout[m]   (up_proj)

@@ -961,7 +961,7 @@ int lc_attn_fwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
   dim3 grid(n_seq * H);
   const float scale = 0.125f;  // 64^-0.5
   static const bool online = [] {
-    const char* e = getenv("LCCLIP_ATTN_FWD_ONLINE");
+    const char* e = lc_diag_env("LCCLIP_ATTN_FWD_ONLINE");
     return !(e && e[0] == '0');
   }();
   switch (nqb) {
@@ -1020,7 +1020,7 @@ int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
   // fused single-pass kernel (dS^T parked in LDS, 1 workgroup per CU) up to 224 keys; the split
   // key-major + query-major pair beyond that (LDS) or when LC_ATTN_BWD_SPLIT=1
   static const int force_split = [] {
-    const char* e = getenv("LC_ATTN_BWD_SPLIT");
+    const char* e = lc_diag_env("LC_ATTN_BWD_SPLIT");
     return e ? atoi(e) : 0;
   }();
   const bool split = force_split != 0;

@@ -1617,7 +1617,7 @@ void plan_tn(TnProb& p, int total_panels) {
   // partials to add atomically); contiguous per-walker chunks instead of block-cyclic 80-88 us
   static int walkers = -1;
   if (walkers < 0) {
-    const char* e = getenv("LC_TN_WALKERS");
+    const char* e = lc_diag_env("LC_TN_WALKERS");
     walkers = e ? atoi(e) : 0;
   }
   const int cus = walkers > 0 ? walkers : cu_count();
@@ -1683,7 +1683,7 @@ SplitK plan_split(int tiles, int units, int min_units, void* ws, long ws_bytes, 
                   long slab_floats = 256 * 256) {
   SplitK sk{tiles, 1, nullptr, nullptr};
   if (g_split_mode < 0) {
-    const char* e = getenv("LC_GEMM_SPLITK");
+    const char* e = lc_diag_env("LC_GEMM_SPLITK");
     g_split_mode = e ? atoi(e) : 1;
   }
   if (!g_split_mode || ws == nullptr) return sk;
@@ -1709,7 +1709,7 @@ SplitK plan_split(int tiles, int units, int min_units, void* ws, long ws_bytes, 
 // N = 768 ones 1-3 % (3 column tiles: the row-major raster already shares B)
 int group_m(int N) {
   static const int forced = [] {
-    const char* e = getenv("LC_GEMM_GM");
+    const char* e = lc_diag_env("LC_GEMM_GM");
     return e ? atoi(e) : 0;
   }();
   if (forced) return forced;
@@ -1786,7 +1786,7 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
   const int units = K / (FP8 ? 128 : 64);
   // (LC_GEMM_SPLIT_MIN overrides the minimum k-tiles per split-K slice: in-step A/Bs)
   static const int split_min = [] {
-    const char* e = getenv("LC_GEMM_SPLIT_MIN");
+    const char* e = lc_diag_env("LC_GEMM_SPLIT_MIN");
     return e && atoi(e) > 0 ? atoi(e) : 8;
   }();
   const SplitK sk = plan_split(tiles, units, split_min, ws, ws_bytes);
@@ -1843,7 +1843,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   auto a = static_cast<const bf16_t*>(A);
   auto b = static_cast<const bf16_t*>(B);
   if (g_force_tile < 0) {
-    const char* e = getenv("LC_GEMM_TILE");
+    const char* e = lc_diag_env("LC_GEMM_TILE");
     g_force_tile = e ? atoi(e) : 0;
   }
   int tile = g_force_tile;
@@ -1874,7 +1874,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     // r_ab_mul_route.txt; before that the 4-wave kernel won, 289 vs 295 us). LC_GEMM_MUL_W4=1
     // routes it to the 4-wave kernel again (A/Bs).
     static const bool mul_w4 = [] {
-      const char* e = getenv("LC_GEMM_MUL_W4");
+      const char* e = lc_diag_env("LC_GEMM_MUL_W4");
       return e && e[0] == '1';
     }();
     if (tile == 8 && epi == EPI_MUL && K <= 1024 && N >= 2048 && mul_w4) tile = 7;

@@ -3,7 +3,21 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "lc_clip.h"
+
+// Schedule-changing environment overrides (tile family, split-K, raster groups, kernel forms)
+// exist for same-box A/B experiments only: they are read in a diagnostic build (make DIAG=1,
+// -DLC_DIAG_ENV). The production library ignores the environment, so a stray variable cannot
+// change the shipped kernels' schedule.
+inline const char* lc_diag_env(const char* name) {
+#ifdef LC_DIAG_ENV
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 typedef uint16_t bf16_t;  // raw bf16 bits in global memory
 typedef short bf16x8 __attribute__((ext_vector_type(8)));

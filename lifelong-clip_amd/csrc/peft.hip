@@ -1302,6 +1302,13 @@ int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, con
   LC_LAUNCH_RET();
 }
 
+static int g_adapter_bwd_fused = 1;
+
+int lc_adapter_bwd_set_form(int fused) {
+  g_adapter_bwd_fused = fused != 0;
+  return LC_OK;
+}
+
 //   dpre = (h > 0) ? scale * (gout Wu) / keep : 0    [M,64]  N = 64, K = D   (B = Wu^T)
 //   dz   = gout + dpre Wd                            [M,D]   N = D,  K = 64  (B = Wd^T)
 int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, const void* h,
@@ -1309,9 +1316,9 @@ int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, con
                    void* dz, long ldz) {
   LC_CHECK_ARG(M > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0);
   LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
-  // one-pass row-block kernel at the towers' widths (LC_ADAPTER_FUSED=0: the two-GEMM form)
-  const char* fe = getenv("LC_ADAPTER_FUSED");  // read per call: tests compare both forms
-  const bool fused = fe == nullptr || atoi(fe) != 0;
+  // one-pass row-block kernel at the towers' widths (lc_adapter_bwd_set_form(0): the two-GEMM
+  // form, which the tests compare it with)
+  const bool fused = g_adapter_bwd_fused != 0;
   // (dpre alone stays on the GEMM: 17.6 vs 22.8 us standalone; with dz 40.4 vs 44.9 us)
   if (fused && dz != nullptr && (D == 768 || D == 512) && M >= 1024 && ((uintptr_t)gout & 15) == 0 &&
       ((uintptr_t)h & 15) == 0 && ((uintptr_t)WuT & 15) == 0 && ((uintptr_t)WdT & 15) == 0) {

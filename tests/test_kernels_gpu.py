@@ -431,13 +431,16 @@ def test_adapter_bwd_fused_matches_gemms(ops, dev, D, M, with_dz, monkeypatch):
     Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
     WuT, WdT = Wu.t().contiguous(), Wd.t().contiguous()
     outs = {}
+    from lcclip import _lib
+    lib = _lib.load()
     for mode in ("1", "0"):
-        monkeypatch.setenv("LC_ADAPTER_FUSED", mode)
+        lib.lc_adapter_bwd_set_form(int(mode))
         dpre = torch.full((M, 64), 7.0, device=dev, dtype=BF)
         dz = torch.full((M, D), 7.0, device=dev, dtype=BF) if with_dz else None
         ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz)
         torch.cuda.synchronize()
         outs[mode] = (dpre, dz)
+    lib.lc_adapter_bwd_set_form(1)
     assert torch.equal(outs["1"][0], outs["0"][0])
     if with_dz:
         assert torch.equal(outs["1"][1], outs["0"][1])
