@@ -1832,8 +1832,9 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
   // epilogue rows are written / side inputs read 8 elements (16 B of bf16) per lane
   LC_CHECK_ARG(ldo0 % 8 == 0 && ldo0 >= N);
-  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets
-  LC_CHECK_ARG(ldo0 <= (1L << 21) && ldo1 <= (1L << 21));
+  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
+  // x ldo x 4 B (f32 outputs) must stay below 2^31 (num_records and the int offsets)
+  LC_CHECK_ARG(ldo0 < (1L << 21) && ldo1 < (1L << 21));
   LC_CHECK_ARG(epi >= 0 && epi <= EPI_AD_ADD);
   if (epi == EPI_GELU || epi == EPI_BF16_F32 || epi == EPI_GELU_D)
     LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
@@ -1934,8 +1935,9 @@ int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* 
                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes) {
   LC_CHECK_ARG(epi >= 0 && epi <= 7);
   LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
-  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets
-  LC_CHECK_ARG(ldo0 <= (1L << 21) && ldo1 <= (1L << 21));
+  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
+  // x ldo x 4 B (f32 outputs) must stay below 2^31 (num_records and the int offsets)
+  LC_CHECK_ARG(ldo0 < (1L << 21) && ldo1 < (1L << 21));
   EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
   return lc_gemm_nt_ex(stream, epi, M, N, K, A, lda, B, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                        aux, ldaux, ep, ws, ws_bytes);
@@ -1968,8 +1970,9 @@ int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void*
   if (epi == EPI_RESID || epi == EPI_MUL || epi == EPI_MUL_Q8)
     LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
   LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
-  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets
-  LC_CHECK_ARG(ldo0 <= (1L << 21) && ldo1 <= (1L << 21));
+  // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
+  // x ldo x 4 B (f32 outputs) must stay below 2^31 (num_records and the int offsets)
+  LC_CHECK_ARG(ldo0 < (1L << 21) && ldo1 < (1L << 21));
   EpiParams ep{nullptr, 0, 1.0f, 1.0f, 0, g_dbg};
   ep.q_scale = q8 ? static_cast<uint8_t*>(q_scale) : nullptr;
   ep.q_rows = q_rows;

@@ -212,7 +212,9 @@ class BlockStack:
     @staticmethod
     def _stage_lora(st, name, A, B, merges):
         """(A_pad [64,K], Bt_pad [64,N]) bf16 with rows >= r zero, staged from A [r,K], B [N,r]
-        by two casts appended to `merges` (launched with the block's weight merges)."""
+        by two casts appended to `merges` (launched with the block's weight merges). The
+        padding rows are zeroed once at allocation and never written (the casts cover rows < r
+        only); the rank-r gradient kernels rely on that (ops.lora_grad_1p)."""
         r, K = A.shape
         N = B.shape[0]
         old = getattr(st, name, None)

@@ -75,8 +75,10 @@ class Fp8Mat:
         pad = (rows + 255) // 256 * 256
         self.rows, self.K = rows, K
         self.data = data if data is not None else torch.empty((rows, K), dtype=FP8, device=device)
-        # rows >= `rows` of the scale buffer are never written: the GEMM reads them only for
-        # tail rows it computes and never stores
+        # rows >= `rows` of the scale buffer (the padding up to 256) carry no meaning: the GEMM
+        # reads them only for tail rows it computes and never stores, and the branch-free
+        # fp8-output GEMM epilogues (EPI_*_Q8) may write arbitrary bytes (0xFF included) there
+        # from clamped tail rows. Only rows < `rows` are valid — never widen a narrow()ed view
         self.scales = scales if scales is not None else torch.empty((K // 128, pad, 4), dtype=FP8,
                                                                    device=device)
 
@@ -353,6 +355,12 @@ def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
     if X.shape[0] != M or a_pad.shape[1] != K or bt_pad.shape[1] != N or a_pad.shape[0] < 16 \
             or bt_pad.shape[0] < 16 or tuple(dA.shape) != (r, K) or tuple(dB.shape) != (N, r):
         raise ValueError("lora_grad_1p: shape mismatch")
+    # the kernel accumulates into dA / dB as dense row-major f32 (+=): anything else would be
+    # silently corrupted. (The zero padding rows >= r of a_pad / bt_pad are the caller's
+    # invariant: BlockStack._stage_lora allocates them zeroed and only ever writes rows < r.)
+    for t, name in ((dA, "dA"), (dB, "dB")):
+        if t.dtype != F32 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError(f"lora_grad_1p: {name} must be a contiguous f32 device tensor")
     ws = splitk_workspace(torch.cuda.current_stream(dY.device))
     call("lc_lora_grad_ws", stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
          ptr(a_pad), a_pad.stride(0), ptr(bt_pad), bt_pad.stride(0), float(scaling), ptr(dA),

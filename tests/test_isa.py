@@ -1,0 +1,61 @@
+"""ISA checks of hand-counted memory waits (CPU: hipcc cross-compiles the device code to gfx950
+assembly; no GPU needed).
+
+adapter_ln_fwd_kernel (peft.hip) waits at the top of each 16-row block with a COUNTED
+`s_waitcnt vmcnt(tail)`: the previous block's stores may stay in flight while the block's
+LDS-DMAs must have landed. CDNA retires vector-memory ops in issue order, so the count is right
+only while the loop issues exactly `tail` stores after its last LDS-DMA — 2 NU + 3 on the waves
+that store everything (NU x_out rows 16 B, NU y rows 8 B, the h block 16 B, mean and rstd
+4 B each). Fewer stores emitted (e.g. two merged) would let a read of a slot whose DMA has not
+landed through, silently; more would only make the wait conservative. This test pins the
+emitted count to the one the kernel source assumes."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "lifelong-clip_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def peft_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC) or shutil.which("make") is None:
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "peft.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    f"-I{os.path.join(ROOT, 'include')}", "--cuda-device-only", "-S",
+                    os.path.join(CSRC, "peft.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    return out.read_text()
+
+
+def function_body(asm, pattern):
+    m = re.search(r"^(" + pattern + r"[^:\s]*):", asm, re.M)
+    assert m, f"kernel {pattern} not found in the assembly"
+    start = m.end()
+    end = asm.index(".Lfunc_end", start)
+    return asm[start:end]
+
+
+@pytest.mark.parametrize("D", [768, 512])
+def test_adapter_ln_fwd_store_tail_matches_wait(peft_asm, D):
+    body = function_body(peft_asm, rf"_ZN12_GLOBAL__N_121adapter_ln_fwd_kernelILi{D}E")
+    lines = [ln.strip() for ln in body.splitlines()]
+    dma = [i for i, ln in enumerate(lines) if ln.startswith("global_load_lds") or
+           (ln.startswith("buffer_load") and " lds" in ln)]
+    assert dma, "no LDS-DMA in the kernel"
+    tail = [ln.split()[0] for ln in lines[dma[-1] + 1:]
+            if ln.startswith(("global_store", "buffer_store"))]
+    NU = D // 8 // 16
+    # x_out (NU x 16 B) + h block (16 B, waves 0-1), y (NU x 8 B), mean / rstd (wave 0)
+    assert tail.count("global_store_dwordx4") == NU + 1, tail
+    assert tail.count("global_store_dwordx2") == NU, tail
+    assert tail.count("global_store_dword") == 2, tail
+    assert len(tail) == 2 * NU + 3, tail
+    # and the counted waits the source derives from it are the ones emitted
+    waits = {int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)}
+    assert {2 * NU, 2 * NU + 1, 2 * NU + 3} <= waits, sorted(waits)

@@ -187,7 +187,12 @@ def _step_vs_oracle(dev, method, B, C, seed, tag):
     probabilities over 100 classes the loss gradient is small, the per-row terms of the adapter
     down-projection gradients (dW_down = sum_rows dpre z^T) mostly cancel, and the bf16-rounding
     oracle is up to 25 % (cosine 0.967) from fp32 on them; the GPU's backward also rounds dpre and
-    dY to bf16 (as the reference's fp16 autocast does), so it sits a little further."""
+    dY to bf16 (as the reference's fp16 autocast does), so it sits a little further.
+    It also fires at config 2's own shape (B = 32, C = 10): measured 7.2e-2 flat vs fp32, worst
+    tensor rel 0.209, min cosine 0.981, where the bf16-rounding oracle is 7.2e-2 / 0.215 / 0.980
+    (profiles/r03/s6/parity_metrics.jsonl). tools/conditioning.py (profiles/r04/) locates it:
+    at B = 32 / C = 10 the image tower's bf16 forward alone is 5.4e-2 from fp32 (text tower
+    exact), at C = 100 the text tower's (1.4e-2 with it exact) — DESIGN.md §2."""
     from lcclip import OnlineTrainer
     cfg = o.VIT_B16
     sd = o.synthetic_state_dict(cfg, method, "both", seed=seed)
@@ -277,10 +282,11 @@ def test_lora_config4_shape_vs_oracle(dev):
     ls = math.exp(sd["logit_scale"].item())
     lg = ls * fi[pick] @ ft.t()
     # The north-star bounds vs fp32 (RMS < 1e-3, max < 2e-3) as everywhere. Against the
-    # bf16-rounding oracle this test bounds the RMS (< 4e-4), not the 8e-4 max of tests/parity.py:
-    # that max was set on 8-logit matrices (B = 2, C = 4), and over this test's 1 600 logits the
-    # largest of the accumulation-order differences is a further tail point (measured 8.6e-4 max
-    # at 3.3e-4 RMS vs fp32, where the bf16-rounding oracle itself is 3.0e-4 RMS from fp32).
+    # bf16-rounding oracle this test bounds the RMS (< 4e-4) and the max at 1e-3 instead of the
+    # 8e-4 max of tests/parity.py: that max was set on 8-logit matrices (B = 2, C = 4), and over
+    # this test's 1 600 logits the largest of the accumulation-order differences is a further
+    # tail point (measured 8.6e-4 max at 3.3e-4 RMS vs fp32, where the bf16-rounding oracle
+    # itself is 3.0e-4 RMS from fp32).
     bmax, brms = logit_errors(lg, ls * i16 @ t16.t(), ls)
     m = dict(img_rel_vs_bf16=rel(fi[pick], i16), txt_rel_vs_bf16=rel(ft, t16),
              img_rel_vs_fp32=rel(fi[pick], i32), txt_rel_vs_fp32=rel(ft, t32),
@@ -296,7 +302,7 @@ def test_lora_config4_shape_vs_oracle(dev):
     assert m["img_rel_vs_bf16"] < 5e-3 and m["txt_rel_vs_bf16"] < 5e-3, m
     assert m["img_rel_vs_fp32"] < 2e-2 and m["txt_rel_vs_fp32"] < 2e-2, m
     check_logits(m)
-    assert m["cos_rms_vs_bf16"] < 4e-4, m
+    assert m["cos_rms_vs_bf16"] < 4e-4 and m["cos_max_vs_bf16"] < 1e-3, m
     assert torch.allclose(probs.sum(-1), torch.ones(B, device=dev), atol=1e-4)
     hi = math.log(C - 1 + math.e)
     assert hi - 1 <= loss.item() <= hi
