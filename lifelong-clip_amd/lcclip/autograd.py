@@ -191,7 +191,7 @@ class _MapleTextFn(torch.autograd.Function):
     model.py:381-395). Gradients: d x0 (to ctx through autograd) and the deep prompts."""
 
     @staticmethod
-    def forward(ctx, tower, tokens, training, save, x0, *deep):
+    def forward(ctx, tower, tokens, training, save, consumer, x0, *deep):
         C, L, D = x0.shape
         replace = {i + 1: (1, d.detach().float().contiguous()) for i, d in enumerate(deep)}
         f, c = tower.forward(tokens, save, training,
@@ -199,16 +199,26 @@ class _MapleTextFn(torch.autograd.Function):
                              replace=replace)
         ctx.tower, ctx.saved_ctx, ctx.shape, ctx.n_deep = tower, c, (C, L, D), len(deep)
         ctx.deep_shapes = [tuple(d.shape) for d in deep]
+        ctx.consumer = consumer
+        if consumer is not None:  # read on the consumer stream (the head)
+            f.record_stream(consumer)
         return f
 
     @staticmethod
     def backward(ctx, df):
+        # autograd runs this on the forward's stream (the text stream when `consumer` is set):
+        # df comes from the consumer stream, the results go back to it
+        if ctx.consumer is not None:
+            df.record_stream(torch.cuda.current_stream(df.device))
         pg = {}
         gx = ctx.tower.backward(ctx.saved_ctx, df.contiguous().float(), {}, prompt_grads=pg,
                                 need_dx=True)
         ctx.saved_ctx = None
         d_deep = [_deep_grad(pg, i + 1, ctx.deep_shapes[i], df) for i in range(ctx.n_deep)]
-        return (None, None, None, None, gx.view(*ctx.shape), *d_deep)
+        if ctx.consumer is not None:
+            for t in (gx, *d_deep):
+                t.record_stream(ctx.consumer)
+        return (None, None, None, None, None, gx.view(*ctx.shape), *d_deep)
 
 
 class _MapleImageFn(torch.autograd.Function):
@@ -239,10 +249,12 @@ class _MapleImageFn(torch.autograd.Function):
         return (None, None, None, None, d_shared, *d_deep)
 
 
-def maple_text_apply(tower, tokens, x0, deep, training):
+def maple_text_apply(tower, tokens, x0, deep, training, consumer=None):
+    """consumer: the stream that reads the features when this runs on another one (MaPLe's text
+    stream); the allocator then keeps the cross-stream tensors alive for it."""
     _check_frozen(tower.stack)
     save = torch.is_grad_enabled() and (x0.requires_grad or any(d.requires_grad for d in deep))
-    return _MapleTextFn.apply(tower, tokens, bool(training), save, x0, *deep)
+    return _MapleTextFn.apply(tower, tokens, bool(training), save, consumer, x0, *deep)
 
 
 def maple_image_apply(tower, img, shared, deep, training):

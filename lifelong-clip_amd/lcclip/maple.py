@@ -56,10 +56,12 @@ class TextEncoder(nn.Module):
         self.dtype = clip_model.dtype
         self._clip = [clip_model]  # not a submodule (the reference does not register it)
 
-    def forward(self, prompts, tokenized_prompts, compound_prompts_deeper_text):
+    def forward(self, prompts, tokenized_prompts, compound_prompts_deeper_text, consumer=None):
+        """consumer: the stream that reads the features, when this runs on another one."""
         x0 = prompts + self.positional_embedding
         return lc_autograd.maple_text_apply(self._clip[0].text_tower, tokenized_prompts, x0,
-                                            list(compound_prompts_deeper_text), self.training)
+                                            list(compound_prompts_deeper_text), self.training,
+                                            consumer=consumer)
 
 
 class MultiModalPromptLearner(nn.Module):
@@ -203,10 +205,44 @@ class MaPLe(nn.Module):
             prefix = self.token_prefix
             suffix = self.token_suffix
         prompts, shared_ctx, deep_text, deep_vision = self.prompt_learner(prefix, suffix)
-        text_features = self.text_encoder(prompts, tokenized_prompts, deep_text)
         vis = self.image_encoder
-        image_features = lc_autograd.maple_image_apply(vis.tower, image, shared_ctx, deep_vision,
-                                                       self.training)
+        side = self._text_stream(image)
+        if side is None:
+            text_features = self.text_encoder(prompts, tokenized_prompts, deep_text)
+            image_features = lc_autograd.maple_image_apply(vis.tower, image, shared_ctx,
+                                                           deep_vision, self.training)
+        else:
+            # The towers are independent until the head: the text tower (C prompts x 77 tokens,
+            # trained through its deep prompts, so never cached) runs on a side stream beside
+            # the image tower, forward and backward (autograd runs each backward on its forward's
+            # stream). The text function is applied after the image one so that its backward
+            # (the higher sequence number) is launched first and overlaps the image backward.
+            main = torch.cuda.current_stream(image.device)
+            ready = torch.cuda.Event()
+            ready.record(main)  # the prompt learner's outputs
+            image_features = lc_autograd.maple_image_apply(vis.tower, image, shared_ctx,
+                                                           deep_vision, self.training)
+            side.wait_event(ready)
+            prompts.record_stream(side)
+            # the deep text prompts are leaves also read on this stream (the visual projections):
+            # hand the text stream views made here, so their gradients from the text stream
+            # join on this one before accumulating into the leaves
+            deep_text = [d.view(d.shape) for d in deep_text]
+            with torch.cuda.stream(side):
+                text_features = self.text_encoder(prompts, tokenized_prompts, deep_text,
+                                                  consumer=main)
+            main.wait_stream(side)
         logits, _, _ = lc_autograd.head_apply(image_features, text_features, self.logit_scale,
                                               probs=False)
         return logits
+
+    # the text tower on its own HIP stream beside the image tower (False: one stream, for A/Bs)
+    overlap_text = True
+
+    def _text_stream(self, image):
+        if not (self.overlap_text and image.is_cuda):
+            return None
+        s = getattr(self, "_side", None)
+        if s is None or s.device != image.device:
+            s = self._side = torch.cuda.Stream(device=image.device)
+        return s
