@@ -278,6 +278,8 @@ def main():
                          "(exercises the collective path; launch through torch.distributed.run)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a HIP graph (1 GPU; measured equal to eager at B=256)")
+    ap.add_argument("--gemm-tile", type=int, default=0,
+                    help="A/B knob: lc_gemm_set_tile value for every GEMM (0 = automatic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -293,6 +295,10 @@ def main():
     torch.cuda.set_device(dev)
 
     from lcclip import AdapterCLIP, OnlineTrainer, ops
+    if args.gemm_tile:
+        from lcclip import _lib
+        if _lib.load().lc_gemm_set_tile(args.gemm_tile) != 0:
+            raise SystemExit(f"--gemm-tile {args.gemm_tile} rejected")
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
     model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev)

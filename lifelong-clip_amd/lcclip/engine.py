@@ -377,7 +377,8 @@ class BlockStack:
 
     # ------------------------------------------------------------------ backward
     def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None,
-                 grad_stream=None, need_dx: bool = True, prompt_grads=None):
+                 grad_stream=None, need_dx: bool = True, prompt_grads=None,
+                 keep_input: bool = False):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
         param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
         have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input.
@@ -397,7 +398,10 @@ class BlockStack:
         prompt tokens the forward appended at that layer (their rows of the layer's input
         gradient; the dropped rows of its output carry zero gradient), and {('R', layer):
         f32 [n_seq, P, D]} for the rows the forward replaced there (those rows' input gradient,
-        which then stops: zeroed below that layer)."""
+        which then stops: zeroed below that layer).
+
+        keep_input: never write into (dx, dxb) (a caller-kept buffer, ImageTower._grad_in); the
+        layers' output gradients then ping-pong between two other pairs."""
         M, D = dx.shape
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
@@ -419,6 +423,8 @@ class BlockStack:
         # output-gradient buffers: the incoming pair and one more (ping-pong); prompt layers
         # expand the current gradient into a free pair and compact their output back
         pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev))]
+        if keep_input:
+            pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev)))
         cur = 0
         # fp8 (no adapter: the block output gradient feeds c_proj dX directly): ln_1's backward
         # also writes its result as the fp8 operand of the next (lower) block's c_proj dX GEMM
@@ -444,8 +450,8 @@ class BlockStack:
                     v[:, L:] = 0
                 cur = e
             gx, gxb = pairs[cur][0][:Mx], pairs[cur][1][:Mx]
-            out = next(i for i in range(len(pairs)) if i != cur and (P == 0 or i != 0 or
-                                                                      pairs[0][0].shape[0] >= Mx))
+            out = next(i for i in range(len(pairs)) if i != cur and (
+                i != 0 or (not keep_input and (P == 0 or pairs[0][0].shape[0] >= Mx))))
             ox, oxb = pairs[out][0][:Mx], pairs[out][1][:Mx]
             # ---- MLP sub-block: x_out = x_mid + [A](c_proj(gelu(c_fc(ln_2(x_mid)))))
             if self.variant == "adapter":
@@ -731,15 +737,30 @@ class ImageTower:
         ops.cast_bf16(df.contiguous(), dfb)
         dln = _empty((n, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
-        dx = torch.zeros((n * L, D), dtype=F32, device=dev)
-        dxb = torch.zeros((n * L, D), dtype=BF16, device=dev)
+        dx, dxb = self._grad_in(n * L, D, dev)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
                                     need_dx=need_dx or 0 in ctx["prompt_layers"],
-                                    prompt_grads=prompt_grads)
+                                    prompt_grads=prompt_grads, keep_input=True)
         return gx if need_dx else None
+
+    def _grad_in(self, rows, D, dev):
+        """The stack-output gradient pair (f32, bf16 [rows, D]): nonzero on the CLS rows only,
+        which ln_post's backward rewrites every step (rows sequence * L: the same for a shape).
+        Kept across steps and never written by the stack backward (keep_input), so it is zeroed
+        once instead of per step (232 MB at B = 256)."""
+        cache = self.__dict__.setdefault("_gin", {})
+        key = (rows, D, dev)
+        buf = cache.get(key)
+        if buf is None:
+            buf = (torch.zeros((rows, D), dtype=F32, device=dev),
+                   torch.zeros((rows, D), dtype=BF16, device=dev))
+            if torch.cuda.is_current_stream_capturing():
+                return buf  # graph-pool memory: not kept beyond this capture
+            cache[key] = buf
+        return buf
 
 
 class TextTower:

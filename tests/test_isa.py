@@ -59,3 +59,33 @@ def test_adapter_ln_fwd_store_tail_matches_wait(peft_asm, D):
     # and the counted waits the source derives from it are the ones emitted
     waits = {int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", body)}
     assert {2 * NU, 2 * NU + 1, 2 * NU + 3} <= waits, sorted(waits)
+
+
+@pytest.fixture(scope="module")
+def gemm_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("isa") / "gemm.s"
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17",
+                    f"-I{os.path.join(ROOT, 'include')}", "--cuda-device-only", "-S",
+                    os.path.join(CSRC, "gemm.hip"), "-o", str(out)],
+                   check=True, capture_output=True)
+    return out.read_text()
+
+
+def test_gemm_kernels_keep_registers(gemm_asm):
+    """The 256x256 GEMM kernels run at the register-file limit (gemm8: 256 VGPRs per wave at two
+    waves per SIMD; the 4-wave kernel: 256 VGPRs + 256 AGPRs): an edit that makes hipcc spill
+    costs 30-70 % on the step shapes without changing a result (r4: a tile loop added to gemm8
+    spilled 312-696 B per lane; fc2 dX 265 -> 459 us). Every instantiation must keep
+    ScratchSize 0, and the 4-wave kernel's main loop must keep its accumulators in AGPRs (no
+    v_accvgpr copies between MFMAs)."""
+    found = 0
+    for m in re.finditer(r"^(_ZN12_GLOBAL__N_1\d+(gemm8_kernel|gemm_w4_kernel|gemm_pp_kernel)"
+                         r"I\w+?EE\w*):", gemm_asm, re.M):
+        end = gemm_asm.index(".Lfunc_end", m.end())
+        tail = gemm_asm[end:end + 4000]
+        scratch = re.search(r"; ScratchSize: (\d+)", tail)
+        assert scratch and int(scratch.group(1)) == 0, f"{m.group(1)} spills: {scratch.group(0)}"
+        found += 1
+    assert found >= 20, found

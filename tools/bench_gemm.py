@@ -69,8 +69,8 @@ for rnd in range(3):
             t = 8 if v in ("f8", "hb") else int(v.rstrip("n"))
             if t in (3, 5, 6, 7, 8) and N % 256:
                 continue
-            if v != "hb":
-                lib.lc_gemm_set_tile(t)
+            if v != "hb" and lib.lc_gemm_set_tile(t) != 0:
+                raise SystemExit(f"lc_gemm_set_tile({t}) rejected")
             a = A[:m, :K]
             b = Bw[:N, :K]
             out0 = o0[:m * N].view(m, N)
