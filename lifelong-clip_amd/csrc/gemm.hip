@@ -471,6 +471,55 @@ struct SplitK {
   int* tickets;   // [T - dp_tiles], zero between launches
 };
 
+// Slice workgroup s_id (0 .. (T - dp) * S - 1, after the dp tiles) -> (tail tile, slice): groups
+// of 8 tail tiles x S slices, slice k of tile x at s_id = 8 S g + x + 8 k, so a tile's slices
+// have equal workgroup ids mod 8 — one XCD under round-robin placement (speed only: the
+// publication below is correct for any placement) — and the last arriver reads the other slabs
+// from its own L2. A last, partial group of Tg < 8 tiles is dealt the same way modulo Tg.
+LC_DEV void splitk_slice(int s_id, int tail_tiles, int S, int& tail, int& split) {
+  const int grp = s_id / (8 * S), rem = s_id % (8 * S);
+  const int tg = min(8, tail_tiles - grp * 8);
+  tail = grp * 8 + rem % tg;
+  split = rem / tg;
+}
+
+// The last-arriving slice's sum of every slice's partial tile, in slice order (bit-identical to
+// adding the S slabs one after another: its own partial, exact in the slab, is taken from the
+// registers instead of re-read). All S <= 4 slabs are addressed through buffer descriptors that
+// are empty for the own slice and for k >= S, so the loads are unconditional (no branch around
+// a load: hipcc would wait vmcnt(0) at every join) and read zero there; CH tiles of every slab in
+// flight per round.
+template <int TM, int TN, int CH>
+LC_DEV void splitk_sum(f32x4 (&acc)[TM][TN], const SplitK& sk, int tail, int split, int lane_off) {
+  constexpr int SLAB = 256 * 256;
+  __amdgpu_buffer_rsrc_t rs[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool use = k < sk.splits && k != split;
+    rs[k] = lc_rsrc(sk.slabs + ((long)tail * sk.splits + (use ? k : 0)) * SLAB,
+                    use ? (long)SLAB * 4 : 0);
+  }
+  static_assert((TM * TN) % CH == 0, "chunking");
+#pragma unroll
+  for (int c = 0; c < TM * TN; c += CH) {
+    f32x4 v[4][CH];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < CH; ++e)
+        v[k][e] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs[k], (lane_off + (c + e) * 256) * 4, 0, 0));
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      f32x4& a = acc[(c + e) / TN][(c + e) % TN];
+      f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sum += (k == split) ? a : v[k][e];  // zero for k >= S
+      a = sum;
+    }
+  }
+}
+
 template <int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
@@ -721,9 +770,10 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
   } else {
-    const int s_id = bid - sk.dp_tiles;
-    split = s_id % sk.splits;
-    bid = sk.dp_tiles + s_id / sk.splits;
+    int tail;
+    splitk_slice(bid - sk.dp_tiles, ((M + BM - 1) / BM) * tiles_n - sk.dp_tiles, sk.splits, tail,
+                 split);
+    bid = sk.dp_tiles + tail;
     const int nt_all = K / KT;
     tb = split * nt_all / sk.splits;
     te = (split + 1) * nt_all / sk.splits;
@@ -984,6 +1034,7 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
       for (int j = 0; j < TN; ++j)
         *reinterpret_cast<f32x4*>(mine + lane_off + (i * TN + j) * 256) = acc[i][j];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(630);
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
@@ -1002,24 +1053,15 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     __syncthreads();
     const int last = flag[0];
     __syncthreads();
+    stamp(631);
     if (!last) {
 #ifdef LC_GEMM_CLOCK
       clock_out();  // a slice that only wrote its slab
 #endif
       return;
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < sk.splits; ++s) {
-      const float* other = sk.slabs + ((long)tail * sk.splits + s) * SLAB;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] += *reinterpret_cast<const f32x4*>(other + lane_off + (i * TN + j) * 256);
-    }
+    splitk_sum<TM, TN, 4>(acc, sk, tail, split, lane_off);
+    stamp(632);
   } else {
     __builtin_amdgcn_s_barrier();  // every wave done with the ring: the epilogue reuses it
   }

@@ -54,6 +54,9 @@ for grp in (0, 1):
     print(f"group {grp}: prologue {s[1] - s[0]} cyc, loop {s[638] - s[1]} cyc "
           f"({(s[638] - s[1]) / nt:.0f}/k-tile), epilogue {s[TN - 1] - s[638]} cyc, "
           f"start offset {s[0] - t0}")
+    if s[630]:
+        print(f"  split slice: slab stores {s[630] - s[638]} | ticket + flag {s[631] - s[630]} | "
+              f"reduce {s[632] - s[631]} | epilogue {s[TN - 1] - s[632]}")
     for p in range(4):
         mf, bw, ld = [], [], []
         for t in range(1, nt - 1):
