@@ -485,7 +485,8 @@ LC_DEV void splitk_slice(int s_id, int tail_tiles, int S, int& tail, int& split)
 
 // The last-arriving slice's sum of every slice's partial tile, in slice order (bit-identical to
 // adding the S slabs one after another: its own partial, exact in the slab, is taken from the
-// registers instead of re-read). All S <= 4 slabs are addressed through buffer descriptors that
+// registers instead of re-read). The slabs are read with sc1 loads (the publication protocol of
+// gemm8_kernel's split path: sc1 stores, no fences). All S <= 4 slabs are addressed through buffer descriptors that
 // are empty for the own slice and for k >= S, so the loads are unconditional (no branch around
 // a load: hipcc would wait vmcnt(0) at every join) and read zero there; CH tiles of every slab in
 // flight per round.
@@ -508,7 +509,7 @@ LC_DEV void splitk_sum(f32x4 (&acc)[TM][TN], const SplitK& sk, int tail, int spl
 #pragma unroll
       for (int e = 0; e < CH; ++e)
         v[k][e] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs[k], (lane_off + (c + e) * 256) * 4, 0, 0));
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs[k], (lane_off + (c + e) * 256) * 4, 0, 16));
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       f32x4& a = acc[(c + e) / TN][(c + e) % TN];
@@ -1026,28 +1027,29 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   if (split >= 0) {
     const int tail = bid - sk.dp_tiles;
     constexpr int SLAB = BM * BN;
-    float* mine = sk.slabs + ((long)tail * sk.splits + split) * SLAB;
     const int lane_off = (wave * TM * TN * 64 + lane) * 4;
+    // publication without fences (MI355X_MICROARCH.md, valid forms: sc1 write-through 16-B slab
+    // stores drained by every wave, a barrier, then one lane's relaxed agent-scope ticket add;
+    // the workgroup whose add returns S-1 reads every other slab with sc1 16-B loads after a
+    // barrier, splitk_sum): no L2 write-back of the XCD's dirty lines (release) and no L1
+    // invalidate (acquire) on the tail's critical path
+    const __amdgpu_buffer_rsrc_t rs_mine =
+        lc_rsrc(sk.slabs + ((long)tail * sk.splits + split) * SLAB, (long)SLAB * 4);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        *reinterpret_cast<f32x4*>(mine + lane_off + (i * TN + j) * 256) = acc[i][j];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lc_u32x4, acc[i][j]), rs_mine,
+                                               (lane_off + (i * TN + j) * 256) * 4, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(630);
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int ticket = __hip_atomic_fetch_add(sk.tickets + tail, 1, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
       const int last = ticket == sk.splits - 1;
-      if (last) {
-        __hip_atomic_store(sk.tickets + tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(sk.tickets + tail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = last;
     }
     __syncthreads();
