@@ -575,8 +575,13 @@ attn_bwd_kernel(int n_items, int L, int H, int D, const bf16_t* __restrict__ qkv
       const auto s1 = __builtin_amdgcn_permlane16_swap(xp[2 * p].y, xp[2 * p + 1].y, false, false);
       typedef unsigned int v4u __attribute__((ext_vector_type(4)));
       const v4u v = v4u{s0[0], s1[0], s0[1], s1[1]};
+#ifdef ATT_KO_STORES  // diagnostic builds only: the stores replaced by a keep-alive (results wrong)
+      asm volatile("" ::"v"(v));
+      (void)rs;
+#else
       __builtin_amdgcn_raw_buffer_store_b128(
           v, rs, r * (int)lddq * 2 + (col0 + 32 * p + 16 * (g & 1) + 8 * (g >> 1)) * 2, 0, 0);
+#endif
     }
   };
   auto put_row = [&](long row, int col0, f32x4 x0, f32x4 x1, f32x4 x2, f32x4 x3, float mul) {
