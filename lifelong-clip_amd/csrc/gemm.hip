@@ -1024,6 +1024,27 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   if (g0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
   stamp(TRACE_STAMPS_LOOP_END);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#ifdef G8_PREFETCH
+  // experiment: touch the first k-tile of the tile workgroup blockIdx.x + 256 will run (the same
+  // XCD under round-robin placement) — one dword per 128-B line, 512 lines — so that its prologue
+  // DMA hits this XCD's L2; the loads are never waited for (no epilogue loads in these forms)
+  if constexpr (!FP8 && (EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_GELU || EPI == EPI_GELU_D)) {
+    const int nb = (int)blockIdx.x + 256;
+    if (split < 0 && nb < sk.dp_tiles) {
+      const int nwg = sk.dp_tiles;
+      const int q = nwg / 8, r = nwg % 8, x = nb % 8, loc = nb / 8;
+      const int b2 = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+      int tm2, tn2;
+      tile_coords(b2, (M + BM - 1) / BM, tiles_n, ep.group_m, tm2, tn2);
+      const bool isA = tid < 256;
+      int row = (isA ? tm2 * BM : tn2 * BN) + (tid & 255);
+      row = min(row, (isA ? M : N) - 1);
+      const char* src = (isA ? A : B) + (long)row * (isA ? lda : ldb);
+      int tmp;
+      asm volatile("global_load_dword %0, %1, off" : "=v"(tmp) : "v"(src) : "memory");
+    }
+  }
+#endif
   if (split >= 0) {
     const int tail = bid - sk.dp_tiles;
     constexpr int SLAB = BM * BN;
