@@ -794,6 +794,22 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
 
   // DMA quarter `kind` of k-tile t: 0 = B rows 0..127, 1 = B rows 128..255, 2 = A rows 0..127
   // (+ scales), 3 = A rows 128..255
+  // Buffer-descriptor DMA: one 32-bit lane offset per piece, fixed for the whole loop, and the
+  // k-tile in the SGPR offset — no per-k-tile 64-bit address VALU and half the address VGPRs of
+  // global_load_lds (same-box: every step shape 2-5 % faster, step +1.4 %). Tile rows past M
+  // read as zero through the range check (computed, never stored).
+  const __amdgpu_buffer_rsrc_t rsA = lc_rsrc(A + (long)m0 * lda, (long)min(M - m0, BM) * lda);
+  const __amdgpu_buffer_rsrc_t rsB = lc_rsrc(B + (long)n0 * ldb, (long)BN * ldb);
+  uint32_t voA[2][2], voB[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = h * 128 + (wave * 2 + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & SWM);
+      voA[h][i] = (uint32_t)(row * lda + c * 16);
+      voB[h][i] = (uint32_t)(row * ldb + c * 16);
+    }
   auto dma = [&](int t, int kind) {
 #ifdef G8_NODMA  // diagnostic builds only: main-loop DMA off (results wrong)
     if (t > 0) return;
@@ -801,19 +817,12 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     char* buf = smem + (t & 1) * BUF;
     const bool isA = kind >= 2;
     const int half = kind & 1;
-    const char* g = isA ? A : B;
-    const long ld = isA ? lda : ldb;
-    const int rows_valid = isA ? M : N;
-    const int r0 = isA ? m0 : n0;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row0 = half * 128 + (wave * 2 + i) * 8;  // one KiB, lane-linear in LDS
-      const int row = row0 + (lane >> 3);
-      const int c = (lane & 7) ^ ((row >> 1) & SWM);
-      int gr = r0 + row;
-      gr = gr < rows_valid ? gr : rows_valid - 1;  // tail rows computed, never stored
-      glds16(g + (long)gr * ld + (long)t * 128 + c * 16,
-             buf + (isA ? 0 : TILE_A) + row0 * 128);
+      const int row0 = half * 128 + (wave * 2 + i) * 8;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rsA : rsB,
+                                               LDS_PTR(buf + (isA ? 0 : TILE_A) + row0 * 128), 16,
+                                               isA ? voA[half][i] : voB[half][i], t * 128, 0, 0);
     }
     if constexpr (FP8) {
       if (kind == 2) {
@@ -1024,27 +1033,6 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   if (g0) __builtin_amdgcn_s_barrier();  // match group 1's stagger barrier
   stamp(TRACE_STAMPS_LOOP_END);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#ifdef G8_PREFETCH
-  // experiment: touch the first k-tile of the tile workgroup blockIdx.x + 256 will run (the same
-  // XCD under round-robin placement) — one dword per 128-B line, 512 lines — so that its prologue
-  // DMA hits this XCD's L2; the loads are never waited for (no epilogue loads in these forms)
-  if constexpr (!FP8 && (EPI == EPI_BF16 || EPI == EPI_F32 || EPI == EPI_GELU || EPI == EPI_GELU_D)) {
-    const int nb = (int)blockIdx.x + 256;
-    if (split < 0 && nb < sk.dp_tiles) {
-      const int nwg = sk.dp_tiles;
-      const int q = nwg / 8, r = nwg % 8, x = nb % 8, loc = nb / 8;
-      const int b2 = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
-      int tm2, tn2;
-      tile_coords(b2, (M + BM - 1) / BM, tiles_n, ep.group_m, tm2, tn2);
-      const bool isA = tid < 256;
-      int row = (isA ? tm2 * BM : tn2 * BN) + (tid & 255);
-      row = min(row, (isA ? M : N) - 1);
-      const char* src = (isA ? A : B) + (long)row * (isA ? lda : ldb);
-      int tmp;
-      asm volatile("global_load_dword %0, %1, off" : "=v"(tmp) : "v"(src) : "memory");
-    }
-  }
-#endif
   if (split >= 0) {
     const int tail = bid - sk.dp_tiles;
     constexpr int SLAB = BM * BN;
@@ -1856,6 +1844,8 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
   }();
   const SplitK sk = plan_split(tiles, units, split_min, ws, ws_bytes);
   const long ea = FP8 ? 1 : 2;  // bytes per element
+  // the main-loop DMA descriptors span one 256-row tile of A / B with 32-bit byte offsets
+  LC_CHECK_ARG(lda * ea < (1L << 23) && ldb * ea < (1L << 23));
   dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
 #define LC_G8_CASE(E)                                                                          \
   case E:                                                                                      \
