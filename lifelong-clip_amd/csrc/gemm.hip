@@ -379,10 +379,30 @@ gemm_nt_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
+  // LDS-DMA through per-tile buffer descriptors (as gemm8_kernel): lane offsets fixed for the
+  // loop, the k-tile in the SGPR offset; tile rows past M read as zero (computed, never stored)
+  constexpr int IA = BM / 8 / NW, IB = BN / 8 / NW;  // 1-KiB pieces per wave and stage
+  static_assert(IA * 8 * NW == BM && IB * 8 * NW == BN, "tile rows must split evenly over the waves");
+  const __amdgpu_buffer_rsrc_t rsA = lc_rsrc(A + (long)m0 * lda, (long)min(M - m0, BM) * lda * 2);
+  const __amdgpu_buffer_rsrc_t rsB = lc_rsrc(B + (long)n0 * ldb, (long)BN * ldb * 2);
+  // (the lane offsets are loop-invariant: hoisted out of the k loop by the compiler. Held in
+  // arrays captured by the lambda instead, hipcc's host pass dropped the kernel's launch stub.)
   auto stage = [&](int buf, int kt) {
     char* s = smem + buf * STAGE_BYTES;
-    stage_tile<BM, NW>(A, lda, m0, M, kt * BK, s, tid);
-    stage_tile<BN, NW>(B, ldb, n0, N, kt * BK, s + BM * 128, tid);
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int r = (wave * IA + i) * 8 + (lane >> 3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, LDS_PTR(s + (wave * IA + i) * 1024), 16,
+                                               (uint32_t)(r * lda * 2 + swz(r, lane & 7) * 16),
+                                               kt * BK * 2, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int r = (wave * IB + i) * 8 + (lane >> 3);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, LDS_PTR(s + BM * 128 + (wave * IB + i) * 1024),
+                                               16, (uint32_t)(r * ldb * 2 + swz(r, lane & 7) * 16),
+                                               kt * BK * 2, 0, 0);
+    }
   };
 
   auto compute = [&](const char* sa) {
@@ -1687,9 +1707,11 @@ template <int BM, int BN, int WM, int WN, int STAGES>
 int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, long lda,
               const bf16_t* B, long ldb, const float* bias, float alpha, void* o0, long l0,
               void* o1, long l1, const void* aux, long la, const EpiParams& ep) {
+  // the main-loop DMA descriptors span one tile of A / B rows with 32-bit byte offsets
+  LC_CHECK_ARG(lda < (1L << 22) && ldb < (1L << 22));
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   dim3 grid(tiles), block(64 * WM * WN);
-#define LC_NT_CASE(E)                                                                         \
+#define LC_NT_CASE(E)                                                                       \
   case E:                                                                                     \
     hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, STAGES, E>), grid, block, 0, st, M, N, \
                        K, A, lda, B, ldb, bias, alpha, o0, l0, o1, l1, aux, la, ep);          \

@@ -1,6 +1,6 @@
 """Adapter forward / backward kernels at the ViT-B/16 step shape (dev tool): lc_adapter_fwd
-(EPI_AD_DOWN + EPI_AD_UP) and lc_adapter_bwd (EPI_AD_MASK + EPI_AD_ADD), HIP-event timing and
-algorithmic bytes / time. LC_GEMM_TILE forces a tile family for the experiment."""
+(EPI_AD_DOWN + EPI_AD_UP), lc_adapter_bwd (EPI_AD_MASK + EPI_AD_ADD) and the fused adapter +
+LayerNorm forward (lc_adapter_ln_fwd), HIP-event timing and algorithmic bytes / time. LC_GEMM_TILE forces a tile family for the experiment."""
 import os
 import sys
 
@@ -45,6 +45,13 @@ down = timeit(lambda: ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, None))
 bwd = timeit(lambda: ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz))
 up_bytes = (M * D * 4 * 2 + M * D * 2 + M * H * 2)
 add_bytes = (M * D * 2 * 2 + M * H * 2)
+gamma, beta = torch.randn(D, device=dev), torch.randn(D, device=dev)
+y = torch.empty(M, D, device=dev, dtype=BF)
+mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+adln = timeit(lambda: ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, 0.9, 1234, resid, xout, h, gamma,
+                                         beta, y, mean, rstd))
+adln_bytes = M * (D * 2 + D * 4 + D * 4 + D * 2 + H * 2 + 8)
+print(f"adapter_ln_fwd {adln:.1f} us ({adln_bytes / adln / 1e6:.2f} TB/s)", flush=True)
 print(f"tile={os.environ.get('LC_GEMM_TILE', 'auto')} adapter_fwd {fwd:.1f} us | bwd mask {down:.1f} us, "
       f"mask+add {bwd:.1f} us -> add {bwd - down:.1f} us ({add_bytes / (bwd - down) / 1e6:.2f} TB/s); "
       f"up-proj side bytes {up_bytes / 1e6:.0f} MB", flush=True)
