@@ -898,11 +898,15 @@ struct AdLnLay {
   static constexpr int XP = XIMG / 1024 / 8;         // resid DMA pieces per wave
   static constexpr int Z_OFF = 0;                    // one z buffer
   static constexpr int X_OFF = ZIMG;                 // two resid buffers
-  static constexpr int RED_OFF = X_OFF + 2 * XIMG;   // [16][64] f32 down partials (K half 1)
-  static constexpr int H_OFF = RED_OFF + 16 * 64 * 4;       // h block bf16 [16][64]
-  static constexpr int ST_OFF = H_OFF + 16 * 64 * 2;        // [2][8][16] f32 row sums
-  static constexpr int PRM_OFF = ST_OFF + 2 * 8 * 16 * 4;   // bu, gamma, beta [3][D], bd [64] f32
-  static constexpr int BYTES = PRM_OFF + (3 * D + 64) * 4;
+  static constexpr int PRM_OFF = X_OFF + 2 * XIMG;   // bu, gamma, beta [3][D], bd [64] f32
+  static constexpr int ST_OFF = PRM_OFF + (3 * D + 64) * 4;  // [2][8][16] f32 row sums
+  static constexpr int RED_OFF = ST_OFF + 2 * 8 * 16 * 4;    // [16][64] f32 down partials (K half 1)
+  static constexpr int H_OFF = RED_OFF + 16 * 64 * 4;        // h block bf16 [16][64]
+  // y staging over RED / H (both dead by then): [16][YSTR] bf16, rows padded by 16 B so that
+  // the 16 rows of a ds_write_b64 group fall on distinct banks
+  static constexpr int YSTR = D * 2 + 16;
+  static constexpr int Y_OFF = RED_OFF;
+  static constexpr int BYTES = RED_OFF + (16 * YSTR > 16 * 64 * 6 ? 16 * YSTR : 16 * 64 * 6);
   static constexpr int KS = D / 32 / 2;              // down-projection k-steps per wave (K half)
   static constexpr int NU = D / 8 / 16;              // up-projection 16-column tiles per wave
   static_assert(BYTES <= 160 * 1024, "LDS");
@@ -995,9 +999,14 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     const int u = (byte >> 5) ^ swz_w(row);
     return lds0 + L::Z_OFF + row * L::ZROW + u * 32 + (byte & 31);
   };
-  // stores issued after the last DMA of a full block, per wave: h (waves 0-1), x_out and y (NU
-  // each), mean and rstd (wave 0)
-  const int tail = 2 * NU + (wave < 2 ? 1 : 0) + (wave == 0 ? 2 : 0);
+  // stores issued after the last DMA of a full block, per wave: h (waves 0-1), mean and rstd
+  // (wave 0), then NST full-row pieces (x_out 2 rows x D x 4 B and y 2 rows x D x 2 B, 1 KiB each)
+#ifdef ADLN_KO  // (the knocked-out stores are not in flight: the counted waits below stay exact)
+  constexpr int NST = ((ADLN_KO & 1) ? 0 : 2 * D / 256) + ((ADLN_KO & 2) ? 0 : D / 256);
+#else
+  constexpr int NST = 2 * D / 256 + D / 256;
+#endif
+  const int tail = NST + (wave < 2 ? 1 : 0) + (wave == 0 ? 2 : 0);
 
   int b = blockIdx.x;
   dma_x(b, 0);
@@ -1010,9 +1019,9 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     const int r0 = b * 16;
     // this block's z and resid landed; the previous block's tail stores may stay in flight
     if (prev_full) {
-      if (tail == 2 * NU + 3) vmcnt_le<2 * NU + 3>();
-      else if (tail == 2 * NU + 1) vmcnt_le<2 * NU + 1>();
-      else vmcnt_le<2 * NU>();
+      if (tail == NST + 3) vmcnt_le<NST + 3>();
+      else if (tail == NST + 1) vmcnt_le<NST + 1>();
+      else vmcnt_le<NST>();
     } else {
       vmcnt_le<0>();
     }
@@ -1108,10 +1117,25 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     if (g == 0) st[wave * 16 + t] = s1;
     lds_barrier();
     const bool live = r0 + t < M;
-    if (live) {
+    // x_out and y leave as whole rows: both are staged in LDS (x_out in this block's resid
+    // buffer, read for the last time above; y over the dead RED / H region) and stored after one
+    // more barrier as 1-KiB contiguous pieces through descriptors over the block's rows < M.
+    // Stored straight from the MFMA layout, every store instruction covered 16 rows x 64 B
+    // (x_out) / 32 B (y): those stores were 45 of the kernel's 105 us (knockout builds).
+    // x_out image: plain [16][D] f32 rows, 16-B chunk c of row r at chunk (c & ~7) | ((c ^ r) & 7)
+    // (the 8 rows of a write group on distinct banks); y image: [16][YSTR] bf16 rows (padded).
+    const uint32_t xs = lds0 + L::X_OFF + buf * L::XIMG;
+    const uint32_t ys = lds0 + L::Y_OFF;
+    {
+      // this lane's 16-B chunk of row t for tile u: c = wave D/32 + 4u + g (wave D/32 is a
+      // multiple of 8), so its swizzled position is a per-lane base for even / odd u plus u x 64 B
+      static_assert((D / 32) % 8 == 0, "wave column block must be whole 128-B groups");
+      const uint32_t xb = xs + t * D * 4 + wave * (D / 32) * 16;
+      const uint32_t x0 = xb + ((g ^ t) & 7) * 16, x1 = xb + (((4 + g) ^ t) & 7) * 16 - 64;
 #pragma unroll
       for (int u = 0; u < NU; ++u)
-        *reinterpret_cast<f32x4*>(xout + (long)(r0 + t) * ldx + wave * (D / 8) + 16 * u + 4 * g) = xo[u];
+        asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"((u & 1) ? x1 : x0), "v"(xo[u]),
+                     "n"(u * 64) : "memory");
     }
     float mean = 0.f;
 #pragma unroll
@@ -1133,19 +1157,63 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
 #pragma unroll
     for (int w = 0; w < 8; ++w) var += st[128 + w * 16 + t];
     const float rstd = rsqrtf(var * (1.0f / D) + 1e-5f);
-    if (live) {
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int col = wave * (D / 8) + 16 * u + 4 * g;
-        float o[4];
+    for (int u = 0; u < NU; ++u) {
+      const int col = wave * (D / 8) + 16 * u + 4 * g;
+      float o[4];
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) o[rr] = xo[u][rr] * rstd * prm[D + col + rr] + prm[2 * D + col + rr];
-        *reinterpret_cast<uint2*>(y + (long)(r0 + t) * ldy + col) =
-            uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
-      }
-      if (wave == 0 && g == 0) {
-        mean_out[r0 + t] = mean;
-        rstd_out[r0 + t] = rstd;
+      for (int rr = 0; rr < 4; ++rr) o[rr] = xo[u][rr] * rstd * prm[D + col + rr] + prm[2 * D + col + rr];
+      const uint2 ov = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+      asm volatile("ds_write_b64 %0, %1 offset:%2"
+                   ::"v"(ys + t * L::YSTR + (wave * (D / 8) + 4 * g) * 2), "v"(ov), "n"(u * 32)
+                   : "memory");
+    }
+    if (live && wave == 0 && g == 0) {
+      mean_out[r0 + t] = mean;
+      rstd_out[r0 + t] = rstd;
+    }
+    lds_barrier();  // both images complete (and every st read done)
+    {
+      const int rows_here = min(16, M - r0);
+      const __amdgpu_buffer_rsrc_t rx = lc_rsrc(xout + (long)r0 * ldx, (long)rows_here * ldx * 4);
+      const __amdgpu_buffer_rsrc_t ry = lc_rsrc(y + (long)r0 * ldy, (long)rows_here * ldy * 2);
+      // wave w: rows 2w, 2w + 1; x_out D / 256 pieces of 64 chunks per row, then y's 2 x 2 D
+      // bytes as D / 256 pieces of 1 KiB — one row (or y) at a time: few registers in flight
+      constexpr int XPR = D / 256;
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        uint4 v[XPR];
+#pragma unroll
+        for (int j = 0; j < XPR; ++j) {
+          if (h < 2) {
+            const int r = 2 * wave + h, c = j * 64 + lane;
+            asm volatile("ds_read_b128 %0, %1"
+                         : "=v"(v[j]) : "v"(xs + r * D * 4 + ((c & ~7) | ((c ^ r) & 7)) * 16));
+          } else {
+            const int bb = j * 1024 + lane * 16, r = 2 * wave + bb / (2 * D), o = bb % (2 * D);
+            asm volatile("ds_read_b128 %0, %1" : "=v"(v[j]) : "v"(ys + r * L::YSTR + o));
+          }
+        }
+        lds_wait0();
+#pragma unroll
+        for (int j = 0; j < XPR; ++j) {
+          const lc_u32x4 d = lc_u32x4{v[j].x, v[j].y, v[j].z, v[j].w};
+          if (h < 2) {
+#if !(defined(ADLN_KO) && (ADLN_KO & 1))  // (diagnostic builds: x_out stores off)
+            const int r = 2 * wave + h, c = j * 64 + lane;
+            __builtin_amdgcn_raw_buffer_store_b128(d, rx, (int)(r * ldx * 4 + c * 16), 0, 0);
+#else
+            asm volatile("" ::"v"(d));
+#endif
+          } else {
+#if !(defined(ADLN_KO) && (ADLN_KO & 2))  // (diagnostic builds: y stores off)
+            const int bb = j * 1024 + lane * 16, r = 2 * wave + bb / (2 * D), o = bb % (2 * D);
+            __builtin_amdgcn_raw_buffer_store_b128(d, ry, (int)(r * ldy * 2 + o), 0, 0);
+#else
+            asm volatile("" ::"v"(d));
+#endif
+          }
+        }
       }
     }
     // st is rewritten by the next block only after its first two barriers
