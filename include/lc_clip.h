@@ -289,7 +289,8 @@ int lc_adapter_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, co
  * lc_adapter_fwd, then y = bf16(LayerNorm(xout) * gamma + beta) (fp32 statistics, eps 1e-5)
  * with mean / rstd [M] saved — the ln_2 of the same block or the ln_1 of the next
  * (model.py:194-200). z, resid and xout cross HBM once (separately: two GEMM launches and a
- * LayerNorm launch re-reading xout). D in {512, 768}. Replaces: Adapter.forward
+ * LayerNorm launch re-reading xout). D in {512, 768}; xout and y 16-B aligned, ldy % 8 == 0
+ * (both are written as whole-row 16-B pieces). Replaces: Adapter.forward
  * (adapter.py:53-72) + the residual (model.py:440-441) + the next ln_x (model.py:194-200). */
 int lc_adapter_ln_fwd(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
                       const float* bd, const void* Wu, const float* bu, float scale, float keep,

@@ -1350,7 +1350,10 @@ int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, con
                       const float* resid, float* xout, long ldx, void* hout,
                       const float* gamma, const float* beta, void* y, long ldy, float* mean,
                       float* rstd) {
-  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldz % 8 == 0 && ldx % 4 == 0 && ldy % 4 == 0);
+  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldz % 8 == 0 && ldx % 4 == 0 && ldy % 8 == 0);
+  // x_out / y leave as 16-B pieces through descriptors over a 16-row block (32-bit offsets)
+  LC_CHECK_ARG(ldx < (1L << 24) && ldy < (1L << 24));
+  LC_CHECK_ARG(((uintptr_t)xout & 15) == 0 && ((uintptr_t)y & 15) == 0);
   LC_CHECK_ARG(ldz >= D && ldx >= D && ldy >= D && keep > 0.f && keep <= 1.f);
   LC_CHECK_ARG(z && Wd && bd && Wu && bu && resid && xout && hout && gamma && beta && y && mean && rstd);
   int dev = 0, cus = 256;
