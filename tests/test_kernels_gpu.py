@@ -662,7 +662,7 @@ def test_lora_grad_one_pass(ops, dev, M, K, N):
                                       (7, 512, 0.9)])
 def test_adapter_ln_fwd_matches_separate(ops, dev, M, D, keep):
     """The fused adapter + LayerNorm forward (lc_adapter_ln_fwd) against the separate
-    lc_adapter_fwd + lc_layernorm_fwd launches on the same inputs: same dropout mask (same
+    lc_adapter_fwd + lc_layernorm_fwd launches and against torch fp32: same dropout mask (same
     seed), x_out / mean / rstd to f32 rounding, h and the LayerNorm output to bf16 rounding
     (the down projection sums K over the waves in a different order, so a bf16 rounding of h
     can flip); ragged M and a tail block of 7 rows."""
@@ -689,3 +689,16 @@ def test_adapter_ln_fwd_matches_separate(ops, dev, M, D, keep):
     assert rel(xo2, xo1) < 1e-5
     assert rel(m2, m1) < 1e-5 and rel(r2, r1) < 1e-5
     assert rel(y2, y1) < 4e-3
+    # and against a torch fp32 restatement of adapter.py:53-72 + model.py:440-441 + the LayerNorm
+    # (the kernel's dropout pattern taken from its h; the up projection on its bf16 h, as the
+    # MFMA operand is): h to bf16 rounding, x_out / statistics to f32 rounding, y to bf16
+    pre = z.float() @ Wd.float().t() + bd
+    h_ref = torch.relu(pre) * (h2 != 0) / keep
+    assert rel(h2.float(), h_ref) < 4e-3
+    xo_ref = x + z.float() + 0.1 * (h2.float() @ Wu.float().t() + bu)
+    assert rel(xo2, xo_ref) < 1e-5
+    mu = xo_ref.mean(1)
+    rs = torch.rsqrt(((xo_ref - mu[:, None]) ** 2).mean(1) + 1e-5)
+    assert rel(m2, mu) < 1e-5 and rel(r2, rs) < 1e-5
+    y_ref = (xo_ref - mu[:, None]) * rs[:, None] * gam + bet
+    assert rel(y2.float(), y_ref) < 4e-3
