@@ -168,6 +168,16 @@ int lc_patchify(hipStream_t stream, int n_img, int res, int patch, const float* 
 int lc_vit_assemble(hipStream_t stream, int n_img, int n_patch, int D, const float* patch,
                     const float* cls, const float* pos, float* x);
 
+/* lc_vit_assemble, then x0 = ln_pre(x) (f32 [n*(np+1), D], the residual stream) and the first
+ * block's y = bf16(ln_1(x0)) with its mean1 / rstd1 [rows], in one pass over the rows (one
+ * launch instead of three; the assembled rows and x0 are not re-read). D in {512, 768, 1024};
+ * x0 and y row-major with stride D. Replaces: model.py:759-766 (+ the first block's ln_1,
+ * model.py:194-200, 233). */
+int lc_vit_embed_ln(hipStream_t stream, int n_img, int n_patch, int D, const float* patch,
+                    const float* cls, const float* pos, const float* ln_pre_w,
+                    const float* ln_pre_b, float* x0, const float* ln1_w, const float* ln1_b,
+                    void* y, float* mean1, float* rstd1);
+
 /* x[c][t] = emb[tokens[c][t]] + pos[t]   (model.py:943-946). */
 int lc_text_embed(hipStream_t stream, int C, int L, int D, const int64_t* tokens,
                   const float* emb, const float* pos, float* x);

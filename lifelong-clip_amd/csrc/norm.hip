@@ -232,6 +232,62 @@ __global__ void vit_assemble_kernel(int n_img, int np, int D, const float* __res
   }
 }
 
+// conv1 output -> CLS / positional embedding -> ln_pre -> the first block's ln_1, one wave per
+// sequence row and every value of the row in registers (model.py:759-766, 194-200): x0 (f32,
+// the residual stream) and ln_1(x0) (bf16, the QKV GEMM operand) with ln_1's statistics. The
+// separate path writes and re-reads the assembled rows and x0 (vit_assemble, ln_pre, ln_1:
+// ≈ 465 MB more HBM traffic at batch 256). Both LayerNorms two-pass, as ln_fwd_kernel.
+template <int V>
+__global__ void __launch_bounds__(256)
+vit_embed_ln_kernel(int rows, int np, const float* __restrict__ patch,
+                    const float* __restrict__ cls, const float* __restrict__ pos,
+                    const float* __restrict__ g_pre, const float* __restrict__ b_pre,
+                    float* __restrict__ x0, const float* __restrict__ g1,
+                    const float* __restrict__ b1, bf16_t* __restrict__ y,
+                    float* __restrict__ mean1, float* __restrict__ rstd1) {
+  constexpr int D = V * 64;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int L = np + 1, n = row / L, t = row % L;
+  float v[V], p[V], ga[V], be[V];
+  if (t == 0) load_row_f32<V>(cls, lane, v);  // wave-uniform
+  else load_row_f32<V>(patch + ((long)n * np + t - 1) * D, lane, v);
+  load_row_f32<V>(pos + (long)t * D, lane, p);
+  load_row_f32<V>(g_pre, lane, ga);
+  load_row_f32<V>(b_pre, lane, be);
+  auto norm = [&](float (&u)[V], float& mean, float& rstd) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += u[i];
+    mean = wave_sum(s) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      u[i] -= mean;
+      q += u[i] * u[i];
+    }
+    rstd = rsqrtf(wave_sum(q) * (1.0f / D) + 1e-5f);
+  };
+  float m0, r0, m1, r1;
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] += p[i];
+  norm(v, m0, r0);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = v[i] * r0 * ga[i] + be[i];
+  store_row_f32<V>(x0 + (long)row * D, lane, v);
+  load_row_f32<V>(g1, lane, ga);
+  load_row_f32<V>(b1, lane, be);
+  norm(v, m1, r1);
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = v[i] * r1 * ga[i] + be[i];
+  store_row_bf16<V>(y + (long)row * D, lane, v);
+  if (lane == 0) {
+    mean1[row] = m1;
+    rstd1[row] = r1;
+  }
+}
+
 // x[c][t] = tok_emb[tokens[c][t]] + pos[t]   (model.py:943-946)
 __global__ void text_embed_kernel(int C, int L, int D, const int64_t* __restrict__ tokens,
                                   const float* __restrict__ emb, const float* __restrict__ pos,
@@ -368,6 +424,26 @@ int lc_vit_assemble(hipStream_t st, int n_img, int n_patch, int D, const float* 
   const long work = (long)n_img * (n_patch + 1) * D / 4;
   hipLaunchKernelGGL(vit_assemble_kernel, dim3(grid_for(work, 256)), dim3(256), 0, st, n_img,
                      n_patch, D, patch, cls, pos, x);
+  LC_LAUNCH_RET();
+}
+
+int lc_vit_embed_ln(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
+                    const float* cls, const float* pos, const float* ln_pre_w,
+                    const float* ln_pre_b, float* x0, const float* ln1_w, const float* ln1_b,
+                    void* y, float* mean1, float* rstd1) {
+  LC_CHECK_ARG(n_img > 0 && n_patch > 0 && (D == 512 || D == 768 || D == 1024));
+  LC_CHECK_ARG(patch && cls && pos && ln_pre_w && ln_pre_b && x0 && ln1_w && ln1_b && y && mean1 &&
+               rstd1);
+  const long rows = (long)n_img * (n_patch + 1);
+  LC_CHECK_ARG(rows < (1L << 31) - 4);
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+#define LC_VE(V)                                                                                 \
+  hipLaunchKernelGGL(vit_embed_ln_kernel<V>, grid, block, 0, st, (int)rows, n_patch, patch, cls,  \
+                     pos, ln_pre_w, ln_pre_b, x0, ln1_w, ln1_b, (bf16_t*)y, mean1, rstd1)
+  if (D == 512) LC_VE(8);
+  else if (D == 768) LC_VE(12);
+  else LC_VE(16);
+#undef LC_VE
   LC_LAUNCH_RET();
 }
 

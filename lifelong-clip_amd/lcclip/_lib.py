@@ -39,6 +39,7 @@ SIGNATURES = {
                              P, P, c_long, P, c_long],
     "lc_patchify": [P, c_int, c_int, c_int, P, P],
     "lc_vit_assemble": [P, c_int, c_int, c_int, P, P, P, P],
+    "lc_vit_embed_ln": [P, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P],
     "lc_text_embed": [P, c_int, c_int, c_int, P, P, P, P],
     "lc_eot_rows": [P, c_int, c_int, P, P],
     "lc_attn_fwd": [P, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int],

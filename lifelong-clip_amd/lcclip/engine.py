@@ -230,7 +230,7 @@ class BlockStack:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False, prompts=None,
-                stop=None, replace=None):
+                stop=None, replace=None, first_ln1=None):
         """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None).
 
         prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
@@ -239,7 +239,9 @@ class BlockStack:
         only (the MVP query pass, models/mvp_clip.py:211-216). replace: optional
         {layer: (row, f32 [P, D] or [n_seq, P, D])} — rows [row, row + P) of every sequence are
         overwritten before that layer (MaPLe's deep compound prompts,
-        models/maple_clip/model.py:352-395)."""
+        models/maple_clip/model.py:352-395). first_ln1: (y bf16 [M, D], mean, rstd) — the first
+        block's ln_1 of x already computed (ops.vit_embed_ln), used when that block runs on x
+        unchanged (no prompt rows appended or replaced there, bf16 operands)."""
         self.stage()
         M, D = x.shape
         H = self.n_head
@@ -287,6 +289,9 @@ class BlockStack:
             else:
                 if ln1_ready is not None:  # written by the previous block's fused adapter
                     mean1, rstd1 = ln1_ready
+                elif (idx == 0 and first_ln1 is not None and P == 0
+                      and not (replace and 0 in replace)):
+                    h1, mean1, rstd1 = first_ln1
                 else:
                     ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
                 self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
@@ -641,14 +646,17 @@ class ImageTower:
         embedding and before ln_pre (MaPLe's shared visual context,
         models/maple_clip/model.py:566-575); L then counts them. keep: dict that receives what
         embed_backward() needs."""
+        pe, n, npch = self._patch_embed(img)
+        return self._embed_tail(pe, n, npch, extra, keep)
+
+    def _patch_embed(self, img):
+        """conv1 as a GEMM on im2col rows: (f32 [n*np, D], n, np)."""
         v = self.visual
         self._stage()
         dev = img.device
         P = v.patch_size
         g = v.input_resolution // P
         npch = g * g
-        L = npch + 1
-        D = v.width
         if img.dim() == 2:
             # conv1's bf16 im2col rows, already produced by the fused train transform
             # (lcclip.transforms.TrainTransform(..., layout="patches"))
@@ -661,8 +669,14 @@ class ImageTower:
             img = img.contiguous().to(F32)
             patches = _empty((n * npch, 3 * P * P), BF16, dev)
             ops.patchify(img, P, patches)
-        pe = _empty((n * npch, D), F32, dev)
+        pe = _empty((n * npch, v.width), F32, dev)
         ops.gemm_nt(patches, self.conv_w, EPI_F32, pe)
+        return pe, n, npch
+
+    def _embed_tail(self, pe, n, npch, extra, keep):
+        v = self.visual
+        dev = pe.device
+        L, D = npch + 1, v.width
         xa = _empty((n * L, D), F32, dev)
         ops.vit_assemble(pe, v.class_embedding, v.positional_embedding, xa, n, npch)
         if extra is not None:
@@ -711,14 +725,39 @@ class ImageTower:
     def forward(self, img, save: bool, training: bool = False, prompts=None):
         """img -> (features f32 [n, E], ctx). prompts: {layer: f32 [n, P, D]} appended before
         that layer (prompt tuning, models/mvp_clip.py:158-175)."""
+        if (self.FUSE_EMBED and not prompts and self.stack.precision == "bf16"
+                and self.visual.width in (512, 768, 1024)):
+            x0, n, L, first = self.embed_ln1(img)
+            return self.forward_embedded(x0, n, L, save, training, prompts, first_ln1=first)
         x0, n, L = self.embed(img)
         return self.forward_embedded(x0, n, L, save, training, prompts)
 
+    # the patch embedding's CLS / positional add, ln_pre and the first ln_1 in one launch
+    # (False: the three separate launches, for A/Bs)
+    FUSE_EMBED = True
+
+    def embed_ln1(self, img):
+        """embed() and the first block's ln_1 in one launch (ops.vit_embed_ln): (x0, n, L,
+        (ln_1(x0) bf16, mean1, rstd1)) for BlockStack.forward(first_ln1=...)."""
+        v = self.visual
+        pe, n, npch = self._patch_embed(img)
+        L, D = npch + 1, v.width
+        dev = pe.device
+        x0 = _empty((n * L, D), F32, dev)
+        y = _empty((n * L, D), BF16, dev)
+        mean1 = _empty((n * L,), F32, dev)
+        rstd1 = _empty((n * L,), F32, dev)
+        ln1 = self.stack.blocks[0].ln_1
+        ops.vit_embed_ln(pe, v.class_embedding, v.positional_embedding, v.ln_pre.weight,
+                         v.ln_pre.bias, ln1.weight, ln1.bias, x0, y, mean1, rstd1, n, npch)
+        return x0, n, L, (y, mean1, rstd1)
+
     def forward_embedded(self, x0, n, L, save: bool, training: bool = False, prompts=None,
-                         replace=None):
+                         replace=None, first_ln1=None):
         """forward() from a precomputed embed() (the MVP query and prompt passes share x0)."""
         self._stage()
-        x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts, replace=replace)
+        x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts, replace=replace,
+                                      first_ln1=first_ln1)
         lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
         f = _empty((n, self.projT.shape[0]), F32, x.device)
         ops.gemm_nt(lnp, self.projT, EPI_F32, f)

@@ -223,6 +223,22 @@ def vit_assemble(patch_emb, cls, pos, x, n_img, n_patch):
     return x
 
 
+def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, mean1, rstd1,
+                 n_img, n_patch):
+    """vit_assemble + ln_pre -> x0 (f32) and the first block's ln_1 -> y (bf16), mean1, rstd1,
+    in one launch (lc_vit_embed_ln)."""
+    D = x0.shape[1]
+    rows = n_img * (n_patch + 1)
+    if tuple(x0.shape) != (rows, D) or tuple(y.shape) != (rows, D) or x0.dtype != F32 \
+            or y.dtype != BF16 or not x0.is_contiguous() or not y.is_contiguous() \
+            or tuple(patch_emb.shape) != (n_img * n_patch, D) or not patch_emb.is_contiguous():
+        raise ValueError("vit_embed_ln: shape / layout mismatch")
+    call("lc_vit_embed_ln", stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
+         ptr(ln_pre_w), ptr(ln_pre_b), ptr(x0), ptr(ln1_w), ptr(ln1_b), ptr(y), ptr(mean1),
+         ptr(rstd1))
+    return x0
+
+
 def text_embed(tokens, emb, pos, x):
     if tokens.dtype != torch.int64 or not tokens.is_contiguous():
         raise ValueError("tokens must be contiguous int64")

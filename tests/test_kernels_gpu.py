@@ -702,3 +702,37 @@ def test_adapter_ln_fwd_matches_separate(ops, dev, M, D, keep):
     assert rel(m2, mu) < 1e-5 and rel(r2, rs) < 1e-5
     y_ref = (xo_ref - mu[:, None]) * rs[:, None] * gam + bet
     assert rel(y2.float(), y_ref) < 4e-3
+
+
+@pytest.mark.parametrize("n,npch,D", [(3, 196, 768), (5, 49, 512), (256, 196, 768)])
+def test_vit_embed_ln_matches_separate(ops, dev, n, npch, D):
+    """lc_vit_embed_ln (CLS / positional embedding + ln_pre + the first block's ln_1 in one
+    launch) against the separate vit_assemble + two layernorm_fwd launches (x0, statistics to
+    f32 rounding, y to bf16 rounding) and against torch fp32
+    (model.py:759-766, 194-200; y to bf16 rounding)."""
+    torch.manual_seed(n + D)
+    L = npch + 1
+    pe = torch.randn(n * npch, D, device=dev)
+    cls = torch.randn(D, device=dev)
+    pos = torch.randn(L, D, device=dev) * 0.1
+    gp, bp = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    g1, b1 = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    x0 = torch.empty(n * L, D, device=dev)
+    y = torch.empty(n * L, D, device=dev, dtype=BF)
+    m1, r1 = torch.empty(n * L, device=dev), torch.empty(n * L, device=dev)
+    ops.vit_embed_ln(pe, cls, pos, gp, bp, g1, b1, x0, y, m1, r1, n, npch)
+    xa = torch.empty(n * L, D, device=dev)
+    ops.vit_assemble(pe, cls, pos, xa, n, npch)
+    x0s = torch.empty_like(x0)
+    ops.layernorm_fwd(xa, gp, bp, x0s, None, None)
+    ys = torch.empty_like(y)
+    m1s, r1s = torch.empty_like(m1), torch.empty_like(r1)
+    ops.layernorm_fwd(x0s, g1, b1, ys, m1s, r1s)
+    assert rel(x0, x0s) < 1e-6 and rel(m1, m1s) < 1e-6 and rel(r1, r1s) < 1e-6
+    assert rel(y, ys) < 1e-3
+    xr = torch.cat([cls[None].expand(n, 1, D), pe.view(n, npch, D)], 1) + pos
+    x0r = torch.nn.functional.layer_norm(xr, (D,), gp, bp, 1e-5).reshape(n * L, D)
+    yr = torch.nn.functional.layer_norm(x0r, (D,), g1, b1, 1e-5)
+    assert rel(x0, x0r) < 1e-5
+    assert rel(y, yr) < 4e-3
+    assert rel(m1, x0r.mean(1)) < 1e-5
