@@ -44,7 +44,9 @@ extern "C" {
 #define LC_EPI_GELU_D_Q8 12 /* out0 bf16 = QuickGELU'(pre); out1 fp8 = QuickGELU(pre)          */
 #define LC_EPI_MUL_Q8 13    /* out1 fp8 = alpha*acc * aux_bf16 (out0 unused)                   */
 
-/* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0.
+/* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0,
+ * lda / ldb (elements) multiples of 8 and below 2^22, ldo0 / ldo1 below 2^21 (the kernels address
+ * a tile's rows through buffer descriptors with 32-bit byte offsets; LC_EINVAL otherwise).
  * Replaces: F.linear for QKV / out-proj (models/clip/lora.py:837, 1072; torch MHA for
  * model.py:217,230), nn.Linear c_fc/c_proj + QuickGELU + residual adds (model.py:219-222,
  * 234-235, 203-206), conv1 as a patch GEMM (model.py:709-713, 756), `@ proj` / `@
