@@ -1907,6 +1907,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
                   void* ws, long ws_bytes) {
   LC_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 64 == 0);
   LC_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0 && lda >= K && ldb >= K);
+  LC_CHECK_ARG(lda < (1L << 22) && ldb < (1L << 22));  // tile descriptors: 32-bit byte offsets
   // epilogue rows are written / side inputs read 8 elements (16 B of bf16) per lane
   LC_CHECK_ARG(ldo0 % 8 == 0 && ldo0 >= N);
   // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
