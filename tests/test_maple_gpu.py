@@ -80,16 +80,23 @@ def test_maple_vit_b16_shapes(dev):
 
 
 # ----------------------------------------------------------------------------- fp8 (config 5)
-def run_case_fp8(cfg, sd, mp, img, tok, y, dev, tag, tol):
+def run_case_fp8(cfg, sd, mp, img, tok, y, dev, tag):
     """MaPLe with precision='fp8' (image tower QKV / c_fc / c_proj on the block-scaled fp8 MFMA,
     forward and input-gradient) vs the oracle's fp8 rounding mode (oracle.fp8_rounding: the same
     e4m3 / E8M0 quantisation at the same GEMM operands, bf16 elsewhere) and vs plain fp32.
     The quantiser and the fp8 GEMM themselves are pinned bit-exactly in tests/test_fp8_gpu.py;
     through a whole tower the two sides' quantiser INPUTS differ by bf16 rounding (different
     accumulation orders), and a 2^-8 input difference flips ~3 % of the e4m3 codes (2^-3
-    steps), so the GPU-vs-fp8-oracle gap is a fraction of the fp8 error itself (measured: 0.56x
-    at ViT-B/16 shapes, 0.58x on the tiny tower). Tolerances per case in `tol` (cosine units of
-    the logits = logit / exp(logit_scale); gradient rel-norm), ~2x the measured values."""
+    steps), so the GPU-vs-fp8-oracle gap is a fraction of the fp8 error itself.
+    Bounds anchored to that error, e = the fp8 oracle's own distance from fp32 (logits: max over
+    the matrix in cosine units = logit / exp(logit_scale); gradients: rel-norm per tensor):
+      logits     GPU vs fp8 oracle < 0.75 e + 1e-3,   GPU vs fp32 < 1.25 e + 1e-3
+      gradients  GPU vs fp8 oracle < 0.90 e + 0.02,   GPU vs fp32 < 1.35 e + 0.02
+    Measured (the GPU side is the same on every box since r3; the oracle's fp8 mode moves a few
+    % with the host's BLAS, e.g. the tiny tower's proj.weight e = 0.1277 on the GPU box, 0.1348
+    in the build container): logits 0.42 / 0.58 e vs the fp8 oracle and 1.05 / 0.90 e vs fp32
+    (ViT-B/16 / tiny); gradients 0.47-0.84 e and 0.90-1.28 e per tensor (the worst, that
+    proj.weight: 0.1075 / 0.1635; profiles/r04/t6/)."""
     from lcclip.maple import MaPLe
     rt8 = o.fp8_rounding()
     with torch.no_grad():
@@ -117,11 +124,15 @@ def run_case_fp8(cfg, sd, mp, img, tok, y, dev, tag, tol):
     for k, name in o.MAPLE_TO_MODULE.items():
         met[f"grad_{k}_rel_fp8"] = rel(params[name].grad, g8[k].grad)
         met[f"grad_{k}_rel_fp32"] = rel(params[name].grad, g32[k].grad)
+        met[f"oracle_fp8_grad_{k}_rel_fp32"] = rel(g8[k].grad, g32[k].grad)
     record(test=tag, **met)
-    assert met["cos_err_vs_fp8"] < tol["cos_fp8"] and met["cos_err_vs_fp32"] < tol["cos_fp32"], met
+    e = met["fp8_oracle_vs_fp32"]
+    assert met["cos_err_vs_fp8"] < 0.75 * e + 1e-3, met
+    assert met["cos_err_vs_fp32"] < 1.25 * e + 1e-3, met
     for k in o.MAPLE_TO_MODULE:
-        assert met[f"grad_{k}_rel_fp8"] < tol["grad_fp8"], (k, met)
-        assert met[f"grad_{k}_rel_fp32"] < tol["grad_fp32"], (k, met)
+        e = met[f"oracle_fp8_grad_{k}_rel_fp32"]
+        assert met[f"grad_{k}_rel_fp8"] < 0.90 * e + 0.02, (k, met)
+        assert met[f"grad_{k}_rel_fp32"] < 1.35 * e + 0.02, (k, met)
 
 
 def test_maple_fp8_tiny(dev):
@@ -129,10 +140,9 @@ def test_maple_fp8_tiny(dev):
     run_case_fp8(cfg, o.synthetic_state_dict(cfg, seed=51), o.maple_params(cfg, seed=4),
                  o.synthetic_images(3, cfg.image_resolution, seed=8),
                  o.synthetic_tokens(4, 77, seed=8, vocab=cfg.vocab_size), torch.tensor([0, 2, 3]),
-                 dev, "maple_fp8_tiny",
-                 # measured: cos 1.2e-2 / 1.8e-2 (the fp8 oracle itself is 2.0e-2 from fp32);
-                 # gradients 0.06-0.11 / 0.10-0.16
-                 dict(cos_fp8=2.5e-2, cos_fp32=4e-2, grad_fp8=0.2, grad_fp32=0.3))
+                 dev, "maple_fp8_tiny")
+    # measured: logits 1.2e-2 / 1.8e-2 (the fp8 oracle itself 2.0e-2 from fp32); gradients
+    # 0.06-0.11 / 0.10-0.16 (the oracle's own 0.10-0.16)
 
 
 def test_maple_fp8_vit_b16_shapes(dev):
@@ -140,10 +150,9 @@ def test_maple_fp8_vit_b16_shapes(dev):
     cfg = o.VIT_B16
     run_case_fp8(cfg, o.synthetic_state_dict(cfg, seed=43), o.maple_params(cfg, seed=3),
                  o.synthetic_images(2, 224, seed=7), o.synthetic_tokens(4, 77, seed=7),
-                 torch.tensor([1, 3]), dev, "maple_fp8_vit_b16",
-                 # measured: cos 2.2e-3 / 3.2e-3 (the fp8 oracle itself is 4.0e-3 from fp32);
-                 # gradients 0.05-0.09 / 0.08-0.14
-                 dict(cos_fp8=5e-3, cos_fp32=8e-3, grad_fp8=0.15, grad_fp32=0.25))
+                 torch.tensor([1, 3]), dev, "maple_fp8_vit_b16")
+    # measured: logits 1.7e-3 / 4.2e-3 (the fp8 oracle itself 4.0e-3 from fp32); gradients
+    # 0.04-0.08 / 0.09-0.14 (the oracle's own 0.08-0.12)
 
 
 def test_maple_fp8_rejects_narrow_tower(dev):
