@@ -92,3 +92,20 @@ def test_gemm_kernels_keep_registers(gemm_asm):
         assert scratch and int(scratch.group(1)) == 0, f"{m.group(1)} spills: {scratch.group(0)}"
         found += 1
     assert found >= 20, found
+
+
+def test_peft_walkers_do_not_spill(peft_asm):
+    """The persistent adapter walkers (adapter_ln_fwd_kernel, adapter_bwd_fused_kernel) count
+    their vector-memory operations by hand in `s_waitcnt vmcnt(n)`. A register spill adds scratch
+    loads and stores to that count. Its reloads also wait vmcnt(0) and drain the DMAs in flight.
+    (r4: a variant with contiguous per-walker row shares spilled 4 B per lane in
+    adapter_ln_fwd<768> — hoisted per-lane DMA addresses — until its DMA lambdas recomputed their
+    lane terms.) Every instantiation keeps ScratchSize 0."""
+    found = 0
+    for m in re.finditer(r"^(_ZN12_GLOBAL__N_1\d+(adapter_ln_fwd_kernel|adapter_bwd_fused_kernel)"
+                         r"I\w+?EE\w*):", peft_asm, re.M):
+        end = peft_asm.index(".Lfunc_end", m.end())
+        scratch = re.search(r"; ScratchSize: (\d+)", peft_asm[end:end + 4000])
+        assert scratch and int(scratch.group(1)) == 0, f"{m.group(1)} spills: {scratch.group(0)}"
+        found += 1
+    assert found == 4, found
