@@ -5,7 +5,8 @@ batch 256 per GPU, 1x MI355X), on synthetic 224x224 images and C = 10 class prom
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--classes C]
                   [--method adapter|lora] [--no-cpu-baseline]
 
-For N > 1 launch with torch.distributed.run (one process per GPU, RCCL); per-GPU work is fixed
+For N > 1 bench.py starts the N ranks itself (torch.distributed.run in a child process, one
+process per GPU, RCCL over xGMI; launching it under torch.distributed.run works too); per-GPU work is fixed
 (weak scaling): images shard by rank, the C prompts are sharded across ranks (features
 all-gathered, dL/dT all-reduced), and the PEFT gradients are all-reduced in per-layer-group
 buckets overlapped with backward (lcclip/dp.py).
@@ -18,10 +19,12 @@ import os
 import sys
 import time
 
-# HIP hardware queues per process: left at the runtime's setting (HIP's default is 4, the GPU
-# box's too) and recorded in the output line. With the process group up the trainer shares one
-# side stream between the text tower and the PEFT weight gradients so that main + side + RCCL fit
-# in 4 queues (OnlineTrainer._merge_side_streams).
+# HIP hardware queues per process: 8 unless set (lcclip's own default, set here too because HIP
+# reads it when the runtime initialises, before lcclip is imported below): main, text-tower,
+# weight-gradient and RCCL streams each on their own queue. Recorded in the output line. With
+# fewer than 6 queues the trainer shares one side stream between the text tower and the PEFT
+# weight gradients (OnlineTrainer._merge_side_streams), which costs 6-12 % (profiles/r05/b/).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "lifelong-clip_amd")):
@@ -264,7 +267,59 @@ def cpu_baseline(seconds_cap=60.0, warmup=2, timed=5):
                       f"{threads} threads ({model})"}
 
 
+def visible_gpu_count():
+    """GPUs this job may use, asked in a child process so that the launching parent never
+    touches the GPU (the ranks it starts must be the first processes to initialise HIP)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        raise SystemExit(f"bench.py: could not count GPUs (rc {r.returncode}): {r.stderr[-400:]}")
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n, argv, port):
+    """One process per GPU on this node through torch.distributed.run (it sets RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR/PORT for each rank; rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n, argv, gpu_count=visible_gpu_count, run=None):
+    """`bench.py --gpus N` started without a launcher (WORLD_SIZE unset): start the N ranks as
+    child processes and return the launcher's exit status (non-zero if any rank failed). This
+    replaces the reference's single-process `nn.DataParallel` (methods/_trainer.py:132, 167-168)
+    with one RCCL rank per GPU. The parent makes no GPU call: it only counts the devices in a
+    child, refuses a job larger than the node, and waits."""
+    import subprocess
+    have = gpu_count()
+    if have < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible on this node")
+    cmd = launch_cmd(n, argv, free_port())
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return (run or subprocess.call)(cmd, env=env)
+
+
 def main():
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        pre.add_argument("--force-dist", action="store_true")
+        a, _ = pre.parse_known_args()
+        if a.gpus < 1:
+            raise SystemExit("--gpus must be >= 1")
+        if a.gpus > 1 or a.force_dist:
+            sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -288,9 +343,14 @@ def main():
     dp = world > 1 or args.force_dist
     if args.force_dist:
         os.environ["LCCLIP_DP_FORCE"] = "1"  # lcclip.dp: collectives even on a one-rank group
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}")
     if dp:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -360,6 +420,7 @@ def main():
             "value": round(total_ips, 2),
             "unit": "images/s",
             "n_gpus": world,
+            "rccl_world": dist.get_world_size() if dp else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),

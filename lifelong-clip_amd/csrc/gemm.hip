@@ -497,6 +497,14 @@ struct SplitK {
 // publication below is correct for any placement) — and the last arriver reads the other slabs
 // from its own L2. A last, partial group of Tg < 8 tiles is dealt the same way modulo Tg.
 LC_DEV void splitk_slice(int s_id, int tail_tiles, int S, int& tail, int& split) {
+#ifdef LC_SPLITK_SPREAD
+  // diagnostic build (make SPREAD=1): slice k of tile x at s_id = S x + k, i.e. a tile's slices
+  // on consecutive workgroups and so on different XCDs, to pin the publication protocol's
+  // cross-XCD case (tests/test_kernels_gpu.py split-K cases under LCCLIP_LIB)
+  tail = s_id / S;
+  split = s_id % S;
+  return;
+#endif
   const int grp = s_id / (8 * S), rem = s_id % (8 * S);
   const int tg = min(8, tail_tiles - grp * 8);
   tail = grp * 8 + rem % tg;

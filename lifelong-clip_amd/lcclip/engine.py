@@ -618,6 +618,37 @@ class BlockStack:
             ops.gemm_tn(dyb, X, self._grad(grads, A), alpha=scaling)
 
 
+class RowGrad:
+    """The stack-output gradient pair (f32, bf16 [rows, D]) of a tower whose head reads a few
+    rows per sequence: the row-gathered LayerNorm backward (ln_post at the CLS rows,
+    model.py:782; ln_final at the EOT rows, model.py:954) writes those rows and every other row
+    is zero. One pair is kept across steps (BlockStack.backward(keep_input=True) never writes
+    it) instead of a per-step full-buffer fill (232 MB at B = 256): before each use the rows the
+    previous use wrote are zeroed again, unless `key` says they are the same rows (the image
+    tower's CLS rows are fixed by (n, L)). A larger shape reallocates; a smaller one uses a
+    prefix whose other rows are zero by the same invariant."""
+
+    def __init__(self):
+        self.buf = None
+        self.prev = None       # int64 rows written by the previous use
+        self.prev_key = None
+
+    def get(self, rows, D, dev, idx, key=None):
+        b = self.buf
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # graph-pool memory: fresh zeros, captured as part of the graph, not kept
+            return (torch.zeros((rows, D), dtype=F32, device=dev),
+                    torch.zeros((rows, D), dtype=BF16, device=dev))
+        if b is None or b[0].shape[0] < rows or b[0].shape[1] != D or b[0].device != dev:
+            self.buf = b = (torch.zeros((rows, D), dtype=F32, device=dev),
+                            torch.zeros((rows, D), dtype=BF16, device=dev))
+        elif self.prev is not None and (key is None or key != self.prev_key):
+            for t in b:
+                t.index_fill_(0, self.prev, 0)
+        self.prev, self.prev_key = idx.to(torch.int64), key
+        return b[0][:rows], b[1][:rows]
+
+
 class ImageTower:
     """VisualTransformer.forward (model.py:755-787) on the engine."""
 
@@ -625,6 +656,7 @@ class ImageTower:
         self.visual = visual
         self.stack = stack
         self._key = None
+        self._grad_in = RowGrad()  # ln_post's backward writes the CLS rows only
 
     def _stage(self):
         v = self.visual
@@ -776,7 +808,7 @@ class ImageTower:
         ops.cast_bf16(df.contiguous(), dfb)
         dln = _empty((n, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
-        dx, dxb = self._grad_in(n * L, D, dev)
+        dx, dxb = self._grad_in.get(n * L, D, dev, ctx["cls_idx"], key=(n, L))
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
@@ -784,22 +816,6 @@ class ImageTower:
                                     need_dx=need_dx or 0 in ctx["prompt_layers"],
                                     prompt_grads=prompt_grads, keep_input=True)
         return gx if need_dx else None
-
-    def _grad_in(self, rows, D, dev):
-        """The stack-output gradient pair (f32, bf16 [rows, D]): nonzero on the CLS rows only,
-        which ln_post's backward rewrites every step (rows sequence * L: the same for a shape).
-        Kept across steps and never written by the stack backward (keep_input), so it is zeroed
-        once instead of per step (232 MB at B = 256)."""
-        cache = self.__dict__.setdefault("_gin", {})
-        key = (rows, D, dev)
-        buf = cache.get(key)
-        if buf is None:
-            buf = (torch.zeros((rows, D), dtype=F32, device=dev),
-                   torch.zeros((rows, D), dtype=BF16, device=dev))
-            if torch.cuda.is_current_stream_capturing():
-                return buf  # graph-pool memory: not kept beyond this capture
-            cache[key] = buf
-        return buf
 
 
 class TextTower:
@@ -809,6 +825,7 @@ class TextTower:
         self.clip = clip
         self.stack = stack
         self._key = None
+        self._grad_in = RowGrad()  # ln_final's backward writes the EOT rows only
 
     def _stage(self):
         c = self.clip
@@ -857,10 +874,9 @@ class TextTower:
         ops.cast_bf16(df.contiguous(), dfb)
         dln = _empty((C, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
-        dx = torch.zeros((C * L, D), dtype=F32, device=dev)
-        dxb = torch.zeros((C * L, D), dtype=BF16, device=dev)
+        dx, dxb = self._grad_in.get(C * L, D, dev, ctx["eot"])
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer,
-                                    need_dx=need_dx, prompt_grads=prompt_grads)
+                                    need_dx=need_dx, prompt_grads=prompt_grads, keep_input=True)
         return gx

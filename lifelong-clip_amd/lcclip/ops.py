@@ -233,6 +233,13 @@ def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, m
             or y.dtype != BF16 or not x0.is_contiguous() or not y.is_contiguous() \
             or tuple(patch_emb.shape) != (n_img * n_patch, D) or not patch_emb.is_contiguous():
         raise ValueError("vit_embed_ln: shape / layout mismatch")
+    # every other operand is read raw by the kernel: f32, contiguous, of the sizes it assumes
+    for name, t, numel in (("mean1", mean1, rows), ("rstd1", rstd1, rows), ("cls", cls, D),
+                           ("pos", pos, (n_patch + 1) * D), ("ln_pre_w", ln_pre_w, D),
+                           ("ln_pre_b", ln_pre_b, D), ("ln1_w", ln1_w, D), ("ln1_b", ln1_b, D)):
+        if t.dtype != F32 or not t.is_contiguous() or t.numel() != numel or t.device != x0.device:
+            raise ValueError(f"vit_embed_ln: {name} must be contiguous f32 with {numel} elements "
+                             f"on {x0.device}")
     call("lc_vit_embed_ln", stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
          ptr(ln_pre_w), ptr(ln_pre_b), ptr(x0), ptr(ln1_w), ptr(ln1_b), ptr(y), ptr(mean1),
          ptr(rstd1))

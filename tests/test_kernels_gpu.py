@@ -419,7 +419,7 @@ def test_adapter_fwd_bwd(ops, dev, D, M, keep):
 
 @pytest.mark.parametrize("D,M,with_dz", [(768, 50432, True), (768, 4109, True), (768, 1031, True),
                                          (512, 2013, True), (768, 4109, False)])
-def test_adapter_bwd_fused_matches_gemms(ops, dev, D, M, with_dz, monkeypatch):
+def test_adapter_bwd_fused_matches_gemms(ops, dev, D, M, with_dz):
     """The one-pass adapter backward (row-block walker, M >= 1024 at D = 768 / 512) gives the
     two-GEMM form's dpre and dz bit for bit (same MFMA operand and k order, same epilogue
     arithmetic): ragged last block, a walker with a single block, the step's row count; and the
@@ -433,14 +433,16 @@ def test_adapter_bwd_fused_matches_gemms(ops, dev, D, M, with_dz, monkeypatch):
     outs = {}
     from lcclip import _lib
     lib = _lib.load()
-    for mode in ("1", "0"):
-        lib.lc_adapter_bwd_set_form(int(mode))
-        dpre = torch.full((M, 64), 7.0, device=dev, dtype=BF)
-        dz = torch.full((M, D), 7.0, device=dev, dtype=BF) if with_dz else None
-        ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz)
-        torch.cuda.synchronize()
-        outs[mode] = (dpre, dz)
-    lib.lc_adapter_bwd_set_form(1)
+    try:
+        for mode in ("1", "0"):
+            lib.lc_adapter_bwd_set_form(int(mode))
+            dpre = torch.full((M, 64), 7.0, device=dev, dtype=BF)
+            dz = torch.full((M, D), 7.0, device=dev, dtype=BF) if with_dz else None
+            ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz)
+            torch.cuda.synchronize()
+            outs[mode] = (dpre, dz)
+    finally:
+        lib.lc_adapter_bwd_set_form(1)  # process-wide: restored even if a launch raised
     assert torch.equal(outs["1"][0], outs["0"][0])
     if with_dz:
         assert torch.equal(outs["1"][1], outs["0"][1])
@@ -704,7 +706,8 @@ def test_adapter_ln_fwd_matches_separate(ops, dev, M, D, keep):
     assert rel(y2.float(), y_ref) < 4e-3
 
 
-@pytest.mark.parametrize("n,npch,D", [(3, 196, 768), (5, 49, 512), (256, 196, 768)])
+@pytest.mark.parametrize("n,npch,D", [(3, 196, 768), (5, 49, 512), (256, 196, 768),
+                                      (2, 256, 1024)])
 def test_vit_embed_ln_matches_separate(ops, dev, n, npch, D):
     """lc_vit_embed_ln (CLS / positional embedding + ln_pre + the first block's ln_1 in one
     launch) against the separate vit_assemble + two layernorm_fwd launches (x0, statistics to

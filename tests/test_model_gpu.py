@@ -138,6 +138,27 @@ def test_module_path_matches_fused_trainer(golden, dev, method):
             assert rel(p.grad, tr.grads[n2[n]]) < 1e-3, n
 
 
+def test_kept_grad_buffers_across_shapes(golden, dev):
+    """The towers keep their stack-output gradient pair across steps (engine.RowGrad: only the
+    CLS / EOT rows are written). Steps whose batch size, prompt count and EOT rows change give
+    the same PEFT gradients as a fresh trainer on each batch (stale rows of another
+    shape must never add gradient)."""
+    from lcclip import OnlineTrainer
+    d, sd = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    steps = [(img, y, tok), (img[:1], y[1:] * 0 + 1, tok[[1, 2]]), (img, y, tok),
+             (img[:1], y[1:], tok[[2, 1]]), (img, y, tok)]
+    tr = OnlineTrainer(make_wrapper(sd, "adapter", "both", dev))
+    for i, (a, b, t) in enumerate(steps):
+        tr.forward_backward(a, b, t)
+        got = tr.flat_g.clone()
+        fresh = OnlineTrainer(make_wrapper(sd, "adapter", "both", dev))
+        fresh.forward_backward(a, b, t)
+        assert rel(got, fresh.flat_g) < 1e-6, i
+
+
 def test_backbone_grad_guard(golden, dev):
     d, sd = golden
     w = make_wrapper(sd, "adapter", "both", dev)

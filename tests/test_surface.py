@@ -160,3 +160,32 @@ def test_maple_surface():
     ids = torch.tensor([[49406 % 512, 5, 6, 7, 8, 9, 511] + [0] * 70])
     tok, pre, suf = m._split(ids)
     assert pre.shape == (1, 1, Dt) and suf.shape == (1, 77 - 1 - 3, Dt)
+
+
+def test_rowgrad_buffer_reuse_zeroes_stale_rows():
+    """engine.RowGrad: one kept gradient pair across batch-size changes; every row
+    the previous use wrote is zero again, whatever the new shape (CPU tensors: no kernels)."""
+    import torch
+    from lcclip.engine import RowGrad
+    rg = RowGrad()
+    dev = torch.device("cpu")
+
+    def use(n, L, D=8, idx=None, key="auto"):
+        idx = torch.arange(n, dtype=torch.int32) * L if idx is None else idx
+        k = (n, L) if key == "auto" else key
+        dx, dxb = rg.get(n * L, D, dev, idx, key=k)
+        assert dx.shape == (n * L, D) and dxb.shape == (n * L, D)
+        zero = torch.ones(n * L, dtype=torch.bool)
+        zero[idx.long()] = False
+        assert not dx[zero].any() and not dxb[zero].any()
+        dx[idx.long()] = 1.0      # what the row-gathered LayerNorm backward writes
+        dxb[idx.long()] = 1.0
+        return dx
+    use(4, 5)
+    use(4, 5)                      # same rows: no refill needed
+    use(3, 6)                      # smaller, different row set: old CLS rows zeroed
+    use(2, 5)
+    d = use(6, 5)                  # larger: reallocated
+    assert d.shape[0] == 30
+    use(2, 7, idx=torch.tensor([3, 9], dtype=torch.int32), key=None)   # EOT-style rows
+    use(2, 7, idx=torch.tensor([4, 12], dtype=torch.int32), key=None)

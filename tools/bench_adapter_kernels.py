@@ -1,6 +1,8 @@
 """Adapter forward / backward kernels at the ViT-B/16 step shape (dev tool): lc_adapter_fwd
 (EPI_AD_DOWN + EPI_AD_UP), lc_adapter_bwd (EPI_AD_MASK + EPI_AD_ADD) and the fused adapter +
-LayerNorm forward (lc_adapter_ln_fwd), HIP-event timing and algorithmic bytes / time. LC_GEMM_TILE forces a tile family for the experiment."""
+LayerNorm forward (lc_adapter_ln_fwd), HIP-event timing and algorithmic bytes / time. LC_GEMM_TILE forces a tile family
+for the experiment ONLY in a diagnostic build (make DIAG=1, selected with LCLIB=<that .so>): the
+production library ignores schedule environment variables, so the tool refuses them without LCLIB."""
 import os
 import sys
 
@@ -10,6 +12,9 @@ import torch  # noqa: E402
 
 from lcclip import _lib, ops  # noqa: E402
 
+if os.environ.get("LC_GEMM_TILE") and not os.environ.get("LCLIB"):
+    raise SystemExit("LC_GEMM_TILE needs a DIAG=1 build selected with LCLIB (the production library "
+                     "ignores it, and the result would be mislabelled)")
 if os.environ.get("LCLIB"):
     _lib.load(os.path.join(ROOT, os.environ["LCLIB"]))
 dev = torch.device("cuda:0")

@@ -1,6 +1,8 @@
 """Adapter weight-gradient microbenchmark (dev tool): lc_adapter_wgrad (dWu, dbu, dWd, dbd in one
 gemm_tn_wide launch) at the ViT-B/16 step shape M = 50 432, D = 768; HIP-event timing, algorithmic
-bytes (gout, z, h, dpre read once) / time. LC_TN_WALKERS overrides the walkers per launch."""
+bytes (gout, z, h, dpre read once) / time. LC_TN_WALKERS overrides the walkers per launch
+ONLY in a diagnostic build (make DIAG=1, selected with LCLIB=<that .so>): the production library
+ignores schedule environment variables, so the tool refuses them without LCLIB."""
 import os
 import sys
 
@@ -10,6 +12,9 @@ import torch  # noqa: E402
 
 from lcclip import _lib, ops  # noqa: E402
 
+if os.environ.get("LC_TN_WALKERS") and not os.environ.get("LCLIB"):
+    raise SystemExit("LC_TN_WALKERS needs a DIAG=1 build selected with LCLIB (the production library "
+                     "ignores it, and the result would be mislabelled)")
 if os.environ.get("LCLIB"):  # an experimental build of the library
     _lib.load(os.path.join(ROOT, os.environ["LCLIB"]))
 
