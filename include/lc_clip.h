@@ -387,6 +387,79 @@ int lc_head_logits(hipStream_t stream, int B, int C, int E, const float* img_n, 
 int lc_softmax_bwd_rows(hipStream_t stream, int B, int C, const float* probs, const float* dprobs,
                         float* dlogits);
 
+/* x [n] f32 *= s, s = 2^(target_exp - floor(log2 max|x|)) computed on the device and written to
+ * scale[0] (1 when max|x| is 0 or not finite): the loss scaling of the IEEE-half text tower's
+ * backward, per call (torch.cuda.amp.GradScaler's role, methods/adapter_clip.py:93). */
+int lc_grad_pow2_normalize(hipStream_t stream, long n, float* x, float* scale, int target_exp);
+
+/* y[i] += x[i] / scale[0] (n elements, f32): the scaled gradients back to their true size. */
+int lc_add_unscaled(hipStream_t stream, long n, float* y, const float* x, const float* scale);
+
+/* ---- IEEE-half storage: the text tower ------------------------------------------------------
+ * Each _f16 entry point is its namesake above with every 16-bit operand, output and weight
+ * image in IEEE half (binary16, round-to-nearest-even) instead of bf16: same arguments, same
+ * shape rules and error codes, f32 operands unchanged; the MFMA is v_mfma_f32_16x16x32_f16.
+ * The reference computes both towers under fp16 autocast (methods/adapter_clip.py:87); the
+ * text tower keeps that precision here (its bf16 rounding carries half of the logits' distance
+ * from fp32 and most of the C = 100 gradients'), the image tower keeps bf16
+ * (BASELINE config 2). Built from the same kernel sources with -DLC_F16. */
+int lc_gemm_nt_f16(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                   void* out1, long ldo1, const void* aux, long ldaux);
+int lc_gemm_nt_ws_f16(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
+                      const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
+                      void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes);
+int lc_gemm_tn_f16(hipStream_t stream, int M, int N1, int N2, const void* A, long lda, const void* B,
+                   long ldb, float alpha, float* C, long ldc, float* colsum, float colsum_scale);
+int lc_gemm_tn_ws_f16(hipStream_t stream, int M, int N1, int N2, const void* A, long lda,
+                      const void* B, long ldb, float alpha, float* C, long ldc, float* colsum,
+                      float colsum_scale, void* ws, long ws_bytes);
+int lc_layernorm_fwd_f16(hipStream_t stream, int rows, int D, const float* x, long ldx,
+                         const int* row_idx, const float* gamma, const float* beta, void* y,
+                         int y_f32, long ldy, float* mean, float* rstd);
+int lc_layernorm_bwd_f16(hipStream_t stream, int rows, int D, const void* dy, int dy_f32, long ldy,
+                         const float* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, float* dx, void* dx_bf16, long ldo,
+                         const int* row_idx);
+int lc_attn_fwd_f16(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq, void* O,
+                    long ldo, float* lse, int causal);
+int lc_attn_bwd_f16(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
+                    const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
+                    int causal);
+int lc_cast_bf16_f16(hipStream_t stream, long n, const float* src, void* dst);
+int lc_merge_weight_f16(hipStream_t stream, int N, int K, int r, const float* W, const float* A,
+                        const float* B, float scaling, void* out, void* outT);
+int lc_cast_weights_bf16_f16(hipStream_t stream, int n, const float* const* W, const int* N,
+                             const int* K, void* const* out, void* const* outT);
+int lc_merge_weights_bf16_f16(hipStream_t stream, int n, const float* const* W, const float* const* A,
+                              const float* const* B, const int* r, const float* scaling, const int* N,
+                              const int* K, void* const* out, void* const* outT);
+int lc_lora_grad_f16(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
+                     const void* X, long ldx, const float* A, const float* B, float scaling,
+                     float* dA, float* dB);
+int lc_lora_grad_ws_f16(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
+                        const void* X, long ldx, const void* apad, long lda, const void* btpad,
+                        long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes);
+int lc_adapter_fwd_f16(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
+                       const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                       unsigned long long seed, const unsigned long long* seed_dev,
+                       const float* resid, float* xout, long ldx, void* h);
+int lc_adapter_ln_fwd_f16(hipStream_t stream, int M, int D, const void* z, long ldz, const void* Wd,
+                          const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                          unsigned long long seed, const unsigned long long* seed_dev,
+                          const float* resid, float* xout, long ldx, void* hout,
+                          const float* gamma, const float* beta, void* y, long ldy, float* mean,
+                          float* rstd);
+int lc_adapter_bwd_f16(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                       const void* WuT, const void* WdT, float scale, float keep, void* dpre,
+                       void* dz, long ldz);
+int lc_adapter_wgrad_f16(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                         const void* z, long ldz, const void* dpre, float scale, float* dWu,
+                         float* dbu, float* dWd, float* dbd);
+int lc_adapter_wgrad_ws_f16(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                            const void* h, const void* z, long ldz, const void* dpre, float scale,
+                            float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1266,7 +1266,7 @@ gemm_w4_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int j = 0; j < TN / 2; ++j)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+        asm volatile(LC_MFMA16_ASM " %0, %1, %2, %0"
                      : "+a"(acc[i][j])
                      : "v"(fb[j]), "v"(fa[i]));
       if (dma) dma_piece(s + 3, i);
@@ -1276,7 +1276,7 @@ gemm_w4_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
       }
 #pragma unroll
       for (int j = TN / 2; j < TN; ++j)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+        asm volatile(LC_MFMA16_ASM " %0, %1, %2, %0"
                      : "+a"(acc[i][j])
                      : "v"(fb[j]), "v"(fa[i]));
     }
@@ -1539,7 +1539,7 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   css[0] = css[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const short one = (short)0x3F80;
+  const short one = LC_ONE16;
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)

@@ -189,6 +189,51 @@ softmax_bwd_kernel(int B, int C, const float* __restrict__ p, const float* __res
     dl[(long)b * C + c] = p[(long)b * C + c] * (dp[(long)b * C + c] - dot);
 }
 
+// ---------------------------------------------------------------- half-precision gradient scale
+// The text tower's backward in IEEE half (lc_*_f16) sees gradients of 1e-9..3e-4 at its 16-bit
+// stores (ViT-B/16, C = 10..100: most below half's normal range, 6.1e-5), so its incoming
+// gradient is scaled first, as the reference's torch.cuda.amp.GradScaler scales the loss
+// (methods/adapter_clip.py:93, _trainer.py:163) — here per call and by a power of two computed
+// on the device from the gradient itself: s = 2^(target - floor(log2 max|x|)), which puts
+// max|x| in [2^target, 2^(target+1)) (the tower's own stores stay within ~1.4x of its input's
+// max, measured: target 10 leaves a 30x margin below half's 65504). A zero or non-finite
+// max gives s = 1. Powers of two make scaling and unscaling exact.
+__global__ void __launch_bounds__(1024)
+grad_pow2_normalize_kernel(long n, float* __restrict__ x, float* __restrict__ s_out, int target) {
+  __shared__ float red[16];
+  __shared__ float s_sh;
+  const int tid = threadIdx.x;
+  float m = 0.f;
+  for (long i = tid; i < n; i += 1024) m = fmaxf(m, fabsf(x[i]));
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.f;
+    for (int w = 0; w < 16; ++w) a = fmaxf(a, red[w]);
+    float s = 1.0f;
+    if (a > 0.f && a <= 3.4e38f) {  // finite, nonzero
+      const int e = (int)((__float_as_uint(a) >> 23) & 0xff) - 127;  // floor(log2 a), normals
+      const int k = min(max(target - e, -126), 127);
+      s = __uint_as_float((uint32_t)(k + 127) << 23);
+    }
+    s_sh = s;
+    s_out[0] = s;
+  }
+  __syncthreads();
+  const float s = s_sh;
+  for (long i = tid; i < n; i += 1024) x[i] *= s;
+}
+
+// y[i] += x[i] / s[0] (s a power of two: exact)
+__global__ void __launch_bounds__(256)
+add_unscaled_kernel(long n, float* __restrict__ y, const float* __restrict__ x,
+                    const float* __restrict__ s) {
+  const float inv = 1.0f / s[0];
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+    y[i] += x[i] * inv;
+}
+
 }  // namespace
 
 extern "C" {
@@ -231,6 +276,22 @@ int lc_softmax_bwd_rows(hipStream_t st, int B, int C, const float* probs, const 
                         float* dlogits) {
   LC_CHECK_ARG(B > 0 && C > 0);
   hipLaunchKernelGGL(softmax_bwd_kernel, dim3(B), dim3(64), 0, st, B, C, probs, dprobs, dlogits);
+  LC_LAUNCH_RET();
+}
+
+int lc_grad_pow2_normalize(hipStream_t st, long n, float* x, float* scale, int target_exp) {
+  LC_CHECK_ARG(n > 0 && x != nullptr && scale != nullptr && target_exp >= -100 &&
+               target_exp <= 100);
+  hipLaunchKernelGGL(grad_pow2_normalize_kernel, dim3(1), dim3(1024), 0, st, n, x, scale,
+                     target_exp);
+  LC_LAUNCH_RET();
+}
+
+int lc_add_unscaled(hipStream_t st, long n, float* y, const float* x, const float* scale) {
+  LC_CHECK_ARG(n > 0 && y != nullptr && x != nullptr && scale != nullptr);
+  const long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(add_unscaled_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)),
+                     dim3(256), 0, st, n, y, x, scale);
   LC_LAUNCH_RET();
 }
 

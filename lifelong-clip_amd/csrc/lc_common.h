@@ -46,6 +46,31 @@ LC_DEV long fp8_scale_index(long row, int kblock, long rows_pad) {
   return ((long)(kblock >> 2) * rows_pad + row) * 4 + (kblock & 3);
 }
 
+// The 16-bit storage type. Every kernel reads, writes and multiplies its 16-bit operands only
+// through the helpers below, so the same sources compile for two storage types:
+//   default: bf16 (the image tower, BASELINE config 2's dtype);
+//   -DLC_F16 (the second object of each 16-bit source, entry points suffixed _f16 by
+//            lc_f16_names.h): IEEE half, the reference's autocast dtype
+//            (methods/adapter_clip.py:87), used by the text tower.
+// The names (bf16_t, bf16x8, bf2f, f2bf, pack2bf) stay those of the default build.
+typedef float lc_f32x2 __attribute__((ext_vector_type(2)));
+#ifdef LC_F16
+typedef _Float16 lc_f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 lc_f16x8 __attribute__((ext_vector_type(8)));
+LC_DEV float bf2f(bf16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+LC_DEV float bf2f_s(short h) { return (float)__builtin_bit_cast(_Float16, h); }
+// fp32 -> half, round to nearest even (overflow to +-inf)
+LC_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (_Float16)f); }
+LC_DEV uint32_t pack2bf(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((lc_f32x2){lo, hi}, lc_f16x2));
+}
+LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(lc_f16x8, a),
+                                                __builtin_bit_cast(lc_f16x8, b), c, 0, 0, 0);
+}
+#define LC_MFMA16_ASM "v_mfma_f32_16x16x32_f16"
+#define LC_ONE16 ((short)0x3C00)  // 1.0
+#else
 LC_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 LC_DEV float bf2f_s(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
 
@@ -56,7 +81,6 @@ LC_DEV bf16_t f2bf(float f) {
 }
 // Two values in one v_cvt_pk_bf16_f32. (Two scalar f2bf + shift/or made hipcc convert pairs in
 // its own order and re-shuffle the halves: 2-3 extra VALU per pair in every bf16 epilogue.)
-typedef float lc_f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 lc_bf16x2 __attribute__((ext_vector_type(2)));
 LC_DEV uint32_t pack2bf(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((lc_f32x2){lo, hi}, lc_bf16x2));
@@ -65,6 +89,9 @@ LC_DEV uint32_t pack2bf(float lo, float hi) {
 LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+#define LC_MFMA16_ASM "v_mfma_f32_16x16x32_bf16"
+#define LC_ONE16 ((short)0x3F80)  // 1.0
+#endif
 
 // Async 16-byte global -> LDS copy; LDS destination = wave-uniform base + lane * 16.
 LC_DEV void glds16(const void* gsrc, void* lds_wave_base) {

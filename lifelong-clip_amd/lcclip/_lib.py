@@ -74,7 +74,18 @@ SIGNATURES = {
     "lc_head_logits": [P, c_int, c_int, c_int, P, P, P, P, P],
     "lc_softmax_bwd_rows": [P, c_int, c_int, P, P, P],
     "lc_head_feat_grad": [P, c_int, c_int, c_int, P, c_long, c_long, P, P, P, P, P, P],
+    "lc_grad_pow2_normalize": [P, c_long, P, P, c_int],
+    "lc_add_unscaled": [P, c_long, P, P, P],
 }
+
+# the IEEE-half (text tower) forms: same arguments (include/lc_clip.h, "IEEE-half storage")
+F16_ENTRY_POINTS = ("lc_gemm_nt", "lc_gemm_nt_ws", "lc_gemm_tn", "lc_gemm_tn_ws",
+                    "lc_layernorm_fwd", "lc_layernorm_bwd", "lc_attn_fwd", "lc_attn_bwd",
+                    "lc_cast_bf16", "lc_merge_weight", "lc_cast_weights_bf16",
+                    "lc_merge_weights_bf16", "lc_lora_grad", "lc_lora_grad_ws", "lc_adapter_fwd",
+                    "lc_adapter_ln_fwd", "lc_adapter_bwd", "lc_adapter_wgrad",
+                    "lc_adapter_wgrad_ws")
+SIGNATURES.update({n + "_f16": SIGNATURES[n] for n in F16_ENTRY_POINTS})
 
 _lib = None
 

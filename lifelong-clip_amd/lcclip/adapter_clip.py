@@ -26,7 +26,7 @@ EOT_TOKEN = 49407
 
 class AdapterCLIP(nn.Module):
     def __init__(self, model_name, peft_method="adapter", peft_encoder="both", device=None,
-                 tokenizer=None, arch_overrides=None):
+                 tokenizer=None, arch_overrides=None, text_precision="fp16"):
         super().__init__()
         self.device = device
         design_details = {
@@ -43,10 +43,23 @@ class AdapterCLIP(nn.Module):
         self.dtype = self.model.dtype
         self.prompt_template = "a bad photo of a {}."
         self._tokenizer = tokenizer
+        self.set_text_precision(text_precision)
+
+    def set_text_precision(self, precision):
+        """The text tower's 16-bit storage: 'fp16' (default; IEEE half, the precision the
+        reference's towers run at under torch.cuda.amp.autocast, methods/adapter_clip.py:87) or
+        'bf16'. The image tower stays bf16 (BASELINE config 2). Extension of the reference
+        surface: the reference has one autocast switch for the whole model."""
+        dt = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(precision)
+        if dt is None:
+            raise ValueError("text_precision must be 'fp16' or 'bf16'")
+        self.model.transformer.engine.set_storage(dt)
+        self.text_precision = precision
+        return self
 
     @classmethod
     def from_state_dict(cls, state_dict, peft_method="adapter", peft_encoder="both", device=None,
-                        tokenizer=None):
+                        tokenizer=None, text_precision="fp16"):
         """Build from an in-memory CLIP state dict (the path clip_loader.load takes for a local
         checkpoint file, clip_loader.py:116-135)."""
         from .model import build_model
@@ -63,7 +76,7 @@ class AdapterCLIP(nn.Module):
         self.dtype = self.model.dtype
         self.prompt_template = "a bad photo of a {}."
         self._tokenizer = tokenizer
-        return self
+        return self.set_text_precision(text_precision)
 
     @property
     def module(self):

@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
-from .ops import BF16, F32
+from .ops import F32
 
 
 def _check_frozen(stack):
@@ -59,7 +59,7 @@ class _StackFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         dy = dy.contiguous().float().clone()
-        dyb = torch.empty(dy.shape, dtype=BF16, device=dy.device)
+        dyb = torch.empty(dy.shape, dtype=ctx.stack.dt, device=dy.device)
         ops.cast_bf16(dy, dyb)
         grads = {p: torch.zeros(p.shape, dtype=F32, device=p.device) for p in ctx.params}
         dx, _ = ctx.stack.backward(ctx.saved_list, dy, dyb, grads, ctx.n_seq, ctx.L)

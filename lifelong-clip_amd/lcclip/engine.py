@@ -34,7 +34,7 @@ import os
 import torch
 
 from . import ops
-from .ops import BF16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_D, EPI_MUL, EPI_RESID
+from .ops import BF16, F16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_D, EPI_MUL, EPI_RESID
 from .ops import EPI_GELU_D_Q8, EPI_MUL_Q8
 
 _seed_counter = itertools.count(1)
@@ -78,6 +78,24 @@ class BlockStack:
         # optional int64 device tensor: RNG epoch added to every dropout seed (graph replay)
         self.seed_dev = None
         self.precision = "bf16"  # 'bf16' | 'fp8' (QKV / c_fc / c_proj on the fp8 MFMA)
+        self.dt = BF16  # 16-bit storage of activations, gradients and staged weights
+
+    def set_storage(self, dtype):
+        """16-bit storage type of the stack: torch.bfloat16 (default) or torch.float16 (IEEE
+        half, the reference's autocast dtype: every kernel of the stack then runs its _f16 entry
+        point, include/lc_clip.h). The staged weights are re-staged in the new type."""
+        if dtype not in (BF16, F16):
+            raise ValueError("storage must be torch.bfloat16 or torch.float16")
+        if dtype == F16 and self.precision != "bf16":
+            raise ValueError("float16 storage is not combined with fp8 GEMMs")
+        if dtype != self.dt:
+            self.dt = dtype
+            for st in self.staged:
+                st.frozen_key = None
+                st.peft_key = None
+                for name in ("lora_in", "lora_out"):
+                    st.__dict__.pop(name, None)
+        return self
 
     # ------------------------------------------------------------------ weight staging
     def trainable_params(self):
@@ -107,14 +125,14 @@ class BlockStack:
             if fkey != st.frozen_key:
                 dev = attn.in_proj_weight.device
                 D = attn.in_proj_weight.shape[1]
-                st.wqkv = _empty((3 * D, D), BF16, dev)
-                st.wqkvT = _empty((D, 3 * D), BF16, dev)
-                st.wo = _empty((D, D), BF16, dev)
-                st.woT = _empty((D, D), BF16, dev)
-                st.wfc = _empty((4 * D, D), BF16, dev)
-                st.wfcT = _empty((D, 4 * D), BF16, dev)
-                st.wpr = _empty((D, 4 * D), BF16, dev)
-                st.wprT = _empty((4 * D, D), BF16, dev)
+                st.wqkv = _empty((3 * D, D), self.dt, dev)
+                st.wqkvT = _empty((D, 3 * D), self.dt, dev)
+                st.wo = _empty((D, D), self.dt, dev)
+                st.woT = _empty((D, D), self.dt, dev)
+                st.wfc = _empty((4 * D, D), self.dt, dev)
+                st.wfcT = _empty((D, 4 * D), self.dt, dev)
+                st.wpr = _empty((D, 4 * D), self.dt, dev)
+                st.wprT = _empty((4 * D, D), self.dt, dev)
                 ops.merge_weight(mlp.c_fc.weight.detach(), None, None, 0.0, st.wfc, st.wfcT)
                 ops.merge_weight(mlp.c_proj.weight.detach(), None, None, 0.0, st.wpr, st.wprT)
                 if self.variant != "lora":
@@ -147,10 +165,10 @@ class BlockStack:
                     dev = ad.down_proj.weight.device
                     D = ad.down_proj.weight.shape[1]
                     H = ad.down_proj.weight.shape[0]
-                    st.wd = _empty((H, D), BF16, dev)
-                    st.wdT = _empty((D, H), BF16, dev)
-                    st.wu = _empty((D, H), BF16, dev)
-                    st.wuT = _empty((H, D), BF16, dev)
+                    st.wd = _empty((H, D), self.dt, dev)
+                    st.wdT = _empty((D, H), self.dt, dev)
+                    st.wu = _empty((D, H), self.dt, dev)
+                    st.wuT = _empty((H, D), self.dt, dev)
                     casts.append((ad.down_proj.weight.detach(), st.wd, st.wdT))
                     casts.append((ad.up_proj.weight.detach(), st.wu, st.wuT))
                     st.peft_key = pkey
@@ -209,8 +227,7 @@ class BlockStack:
             return ops.gemm_nt_fp8(ops.quant_fp8(A), st.q[name], epi, out0, **kw)
         return ops.gemm_nt(A, getattr(st, name), epi, out0, **kw)
 
-    @staticmethod
-    def _stage_lora(st, name, A, B, merges):
+    def _stage_lora(self, st, name, A, B, merges):
         """(A_pad [64,K], Bt_pad [64,N]) bf16 with rows >= r zero, staged from A [r,K], B [N,r]
         by two casts appended to `merges` (launched with the block's weight merges). The
         padding rows are zeroed once at allocation and never written (the casts cover rows < r
@@ -219,10 +236,10 @@ class BlockStack:
         N = B.shape[0]
         old = getattr(st, name, None)
         dev = A.device
-        if old is None or old[0].shape[1] != K or old[1].shape[1] != N:
-            old = (torch.zeros((64, K), dtype=BF16, device=dev),
-                   torch.zeros((64, N), dtype=BF16, device=dev),
-                   _empty((N, r), BF16, dev))
+        if old is None or old[0].shape[1] != K or old[1].shape[1] != N or old[0].dtype != self.dt:
+            old = (torch.zeros((64, K), dtype=self.dt, device=dev),
+                   torch.zeros((64, N), dtype=self.dt, device=dev),
+                   _empty((N, r), self.dt, dev))
         a_pad, bt_pad, scratch = old
         merges.append((A.detach(), None, None, 0.0, a_pad[:r], None))
         merges.append((B.detach(), None, None, 0.0, scratch, bt_pad[:r]))
@@ -248,11 +265,11 @@ class BlockStack:
         dev = x.device
         P_of = {int(i): int(t.shape[1]) for i, t in (prompts or {}).items()}
         Mmax = n_seq * (L + max(P_of.values(), default=0))
-        tmp_h = _empty((Mmax, D), BF16, dev)
+        tmp_h = _empty((Mmax, D), self.dt, dev)
         q_g = ops.Fp8Mat(Mmax, 4 * D, dev) if self._fused_q8() else None
         q_h = ops.Fp8Mat(Mmax, D, dev) if self._fused_q8(2) else None  # ln_1 / ln_2 out, fp8
-        tmp_g = _empty((Mmax, 4 * D), BF16, dev) if q_g is None else None
-        tmp_pre = None if save else _empty((Mmax, 4 * D), BF16, dev)
+        tmp_g = _empty((Mmax, 4 * D), self.dt, dev) if q_g is None else None
+        tmp_pre = None if save else _empty((Mmax, 4 * D), self.dt, dev)
         saved = [] if save else None
         # bf16 adapter towers: each adapter runs fused with the LayerNorm that reads its output
         # (ops.adapter_ln_fwd: ln_2 of the block, ln_1 of the next one); ln1_ready carries the
@@ -280,8 +297,8 @@ class BlockStack:
             s = {}
             mean1 = _empty((Mx,), F32, dev)
             rstd1 = _empty((Mx,), F32, dev)
-            h1 = _empty((Mx, D), BF16, dev) if (save and self.variant == "lora") else th
-            qkv = _empty((Mx, 3 * D), BF16, dev)
+            h1 = _empty((Mx, D), self.dt, dev) if (save and self.variant == "lora") else th
+            qkv = _empty((Mx, 3 * D), self.dt, dev)
             if q_h is not None:  # bf16 h1 only when LoRA's gradient reads it
                 qa = ops.layernorm_fwd_fp8(x, blk.ln_1.weight, blk.ln_1.bias, q_h.narrow(Mx),
                                            mean1, rstd1, y=None if h1 is th else h1)
@@ -296,7 +313,7 @@ class BlockStack:
                     ops.layernorm_fwd(x, blk.ln_1.weight, blk.ln_1.bias, h1, mean1, rstd1)
                 self._gemm(st, "wqkv", h1, EPI_BF16, qkv, bias=blk.attn.in_proj_bias)
             ln1_ready = None
-            O = _empty((Mx, D), BF16, dev)
+            O = _empty((Mx, D), self.dt, dev)
             lse = _empty((n_seq * H, Lx), F32, dev)
             ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
             x_mid = _empty((Mx, D), F32, dev)
@@ -304,9 +321,9 @@ class BlockStack:
                 ad = blk.adaptmlp
                 keep = 1.0 - ad.dropout if (training and ad.dropout > 0) else 1.0
                 seed1 = next(_seed_counter) * 0x9E3779B1
-                z1 = _empty((Mx, D), BF16, dev)
+                z1 = _empty((Mx, D), self.dt, dev)
                 ops.gemm_nt(O, st.wo, EPI_BF16, z1, bias=blk.attn.out_proj.bias)
-                hd1 = _empty((Mx, ad.down_size), BF16, dev)
+                hd1 = _empty((Mx, ad.down_size), self.dt, dev)
                 mean2 = _empty((Mx,), F32, dev)
                 rstd2 = _empty((Mx,), F32, dev)
                 if fuse_ln and q_g is None:
@@ -324,7 +341,7 @@ class BlockStack:
                 mean2 = _empty((Mx,), F32, dev)
                 rstd2 = _empty((Mx,), F32, dev)
                 ln2_done = False
-            pre = _empty((Mx, 4 * D), BF16, dev) if save else tmp_pre[:Mx]
+            pre = _empty((Mx, 4 * D), self.dt, dev) if save else tmp_pre[:Mx]
             # training saves QuickGELU'(pre) (the c_fc dX epilogue is then a plain multiply)
             if q_g is not None:
                 # ln_2 and QuickGELU(pre) only as the fp8 operands of c_fc / c_proj (inference
@@ -348,9 +365,9 @@ class BlockStack:
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 seed2 = next(_seed_counter) * 0x9E3779B1
-                z2 = _empty((Mx, D), BF16, dev)
+                z2 = _empty((Mx, D), self.dt, dev)
                 wpr(EPI_BF16, z2, bias=blk.mlp.c_proj.bias)
-                hd2 = _empty((Mx, ad.down_size), BF16, dev)
+                hd2 = _empty((Mx, ad.down_size), self.dt, dev)
                 nxt = idx + 1
                 if (fuse_ln and nxt < len(self.blocks) and (stop is None or nxt < stop)
                         and not P_of.get(nxt, 0) and not P and not (replace and nxt in replace)):
@@ -418,18 +435,18 @@ class BlockStack:
         # the attention backward's dq|dk|dv as the fp8 QKV dX operand (LoRA reads them in bf16)
         fuse_attn = self._fused_q8(3) and self.variant != "lora" and Mmax // n_seq <= 224
         q_dqkv = ops.Fp8Mat(Mmax, 3 * D, dev) if fuse_attn else None
-        da = _empty((Mmax, 4 * D), BF16, dev) if q_da is None else None
-        dh = _empty((Mmax, D), BF16, dev)
-        dO = _empty((Mmax, D), BF16, dev)
-        dqkv = _empty((Mmax, 3 * D), BF16, dev)
-        dz = _empty((Mmax, D), BF16, dev) if self.variant == "adapter" else None
+        da = _empty((Mmax, 4 * D), self.dt, dev) if q_da is None else None
+        dh = _empty((Mmax, D), self.dt, dev)
+        dO = _empty((Mmax, D), self.dt, dev)
+        dqkv = _empty((Mmax, 3 * D), self.dt, dev)
+        dz = _empty((Mmax, D), self.dt, dev) if self.variant == "adapter" else None
         dx_mid = _empty((Mmax, D), F32, dev)
-        dx_midb = _empty((Mmax, D), BF16, dev)
+        dx_midb = _empty((Mmax, D), self.dt, dev)
         # output-gradient buffers: the incoming pair and one more (ping-pong); prompt layers
         # expand the current gradient into a free pair and compact their output back
-        pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev))]
+        pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev))]
         if keep_input:
-            pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev)))
+            pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
         cur = 0
         # fp8 (no adapter: the block output gradient feeds c_proj dX directly): ln_1's backward
         # also writes its result as the fp8 operand of the next (lower) block's c_proj dX GEMM
@@ -446,7 +463,7 @@ class BlockStack:
             Mx = n_seq * Lx
             if P:
                 if len(pairs) == 2:
-                    pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), BF16, dev)))
+                    pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
                 e = 2 if cur != 2 else 1
                 q_of.clear()
                 for src, dst in zip(pairs[cur], pairs[e]):
@@ -574,7 +591,7 @@ class BlockStack:
     def _adapter_bwd(self, blk, st, gout, h, z, keep, dz, grads):
         ad = blk.adaptmlp
         M = gout.shape[0]
-        dpre = _empty((M, ad.down_size), BF16, gout.device)
+        dpre = _empty((M, ad.down_size), self.dt, gout.device)
         ops.adapter_bwd(gout, h, st.wuT, st.wdT, ad.scale, keep, dpre, dz)  # dz None: dpre only
         with self._side():
             if getattr(self, "_gs", None) is not None:
@@ -606,8 +623,8 @@ class BlockStack:
                                  self._grad(grads, B))
             return
         with self._side():
-            xa = _empty((M, 64), BF16, dY.device)
-            dyb = _empty((M, 64), BF16, dY.device)
+            xa = _empty((M, 64), self.dt, dY.device)
+            dyb = _empty((M, 64), self.dt, dY.device)
             gs = getattr(self, "_gs", None)
             if gs is not None:
                 xa.record_stream(gs)
@@ -633,15 +650,16 @@ class RowGrad:
         self.prev = None       # int64 rows written by the previous use
         self.prev_key = None
 
-    def get(self, rows, D, dev, idx, key=None):
+    def get(self, rows, D, dev, idx, key=None, dt=BF16):
         b = self.buf
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
             # graph-pool memory: fresh zeros, captured as part of the graph, not kept
             return (torch.zeros((rows, D), dtype=F32, device=dev),
-                    torch.zeros((rows, D), dtype=BF16, device=dev))
-        if b is None or b[0].shape[0] < rows or b[0].shape[1] != D or b[0].device != dev:
+                    torch.zeros((rows, D), dtype=dt, device=dev))
+        if (b is None or b[0].shape[0] < rows or b[0].shape[1] != D or b[0].device != dev
+                or b[1].dtype != dt):
             self.buf = b = (torch.zeros((rows, D), dtype=F32, device=dev),
-                            torch.zeros((rows, D), dtype=BF16, device=dev))
+                            torch.zeros((rows, D), dtype=dt, device=dev))
         elif self.prev is not None and (key is None or key != self.prev_key):
             for t in b:
                 t.index_fill_(0, self.prev, 0)
@@ -829,12 +847,12 @@ class TextTower:
 
     def _stage(self):
         c = self.clip
-        key = _key(c.text_projection)
+        key = _key(c.text_projection) + (self.stack.dt,)
         if key != self._key:
             P = c.text_projection
             dev = P.device
-            self.projT = _empty((P.shape[1], P.shape[0]), BF16, dev)
-            self.proj = _empty(tuple(P.shape), BF16, dev)
+            self.projT = _empty((P.shape[1], P.shape[0]), self.stack.dt, dev)
+            self.proj = _empty(tuple(P.shape), self.stack.dt, dev)
             ops.merge_weight(P.detach(), None, None, 0.0, self.proj, self.projT)
             self._key = key
 
@@ -855,7 +873,7 @@ class TextTower:
         x, saved = self.stack.forward(x0, C, L, save, training, replace=replace)
         eot = _empty((C,), torch.int32, dev)
         ops.eot_rows(tokens, eot)
-        lnf = _empty((C, D), BF16, dev)
+        lnf = _empty((C, D), self.stack.dt, dev)
         mean = _empty((C,), F32, dev)
         rstd = _empty((C,), F32, dev)
         ops.layernorm_fwd(x, c.ln_final.weight, c.ln_final.bias, lnf, mean, rstd, row_idx=eot)
@@ -865,18 +883,71 @@ class TextTower:
         return f, ctx
 
     def backward(self, ctx, df, grads, on_layer=None, prompt_grads=None, need_dx=False):
-        """Returns the input-embedding gradient (f32 [C*L, D]) when need_dx, else None."""
+        """Returns the input-embedding gradient (f32 [C*L, D]) when need_dx, else None.
+
+        IEEE-half storage (stack.set_storage(torch.float16)): the backward's gradients are
+        mostly below half's normal range (1e-9..3e-4 at ViT-B/16), so the incoming feature
+        gradient is first scaled by a power of two computed on the device
+        (ops.grad_pow2_normalize: the reference's GradScaler role, methods/adapter_clip.py:93),
+        the stack's PEFT gradients are accumulated into a zeroed scratch buffer and added to
+        `grads` divided by that scale (exact)."""
         c = self.clip
         dev = df.device
         C, L = ctx["C"], ctx["L"]
         D = c.transformer.width
-        dfb = _empty(df.shape, BF16, dev)
-        ops.cast_bf16(df.contiguous(), dfb)
+        dt = self.stack.dt
+        scale = out_grads = None
+        df = df.contiguous()
+        if dt == F16:
+            if need_dx or prompt_grads is not None:
+                raise NotImplementedError("float16 text-tower storage with input / prompt "
+                                          "gradients (MaPLe keeps the bf16 text tower)")
+            df = df.float().clone()
+            scale = _empty((1,), F32, dev)
+            ops.grad_pow2_normalize(df, scale)
+            out_grads, grads = grads, self._scratch_grads(dev)
+        dfb = _empty(df.shape, dt, dev)
+        ops.cast_bf16(df, dfb)
         dln = _empty((C, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
-        dx, dxb = self._grad_in.get(C * L, D, dev, ctx["eot"])
+        dx, dxb = self._grad_in.get(C * L, D, dev, ctx["eot"], dt=dt)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer,
                                     need_dx=need_dx, prompt_grads=prompt_grads, keep_input=True)
+        if scale is not None:
+            self._add_unscaled(out_grads, grads, scale)
         return gx
+
+    def _scratch_grads(self, dev):
+        """Zeroed f32 gradient buffers for the stack's PEFT parameters, views of one flat
+        buffer in parameter order."""
+        params = self.stack.trainable_params()
+        flat = torch.zeros(sum(p.numel() for p in params), dtype=F32, device=dev)
+        out, off = {}, 0
+        for p in params:
+            out[p] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self._scratch_flat = flat
+        return out
+
+    def _add_unscaled(self, dst, src, scale):
+        """dst[p] += src[p] / scale: one launch when dst's buffers are consecutive views of one
+        flat buffer in parameter order (the trainer's flat gradient), else one per parameter."""
+        params = self.stack.trainable_params()
+        views = [dst[p] for p in params]
+        first = views[0]
+        contiguous = all(v.is_contiguous() for v in views)
+        off = 0
+        for v in views:
+            if not contiguous or v.data_ptr() != first.data_ptr() + off * 4:
+                contiguous = False
+                break
+            off += v.numel()
+        if contiguous:
+            n = self._scratch_flat.numel()
+            span = torch.as_strided(first, (n,), (1,))
+            ops.add_unscaled(span, self._scratch_flat, scale)
+            return
+        for p in params:
+            ops.add_unscaled(dst[p], src[p], scale)

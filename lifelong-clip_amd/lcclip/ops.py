@@ -7,18 +7,30 @@ import torch
 from ._lib import call, ptr, stream_of
 
 BF16 = torch.bfloat16
+F16 = torch.float16
 F32 = torch.float32
+HALF = (BF16, F16)  # the 16-bit storage types (bf16: image tower; IEEE half: text tower)
 
 EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32, EPI_GELU_D, EPI_MUL = range(8)
 EPI_GELU_D_Q8, EPI_MUL_Q8 = 12, 13  # gemm_nt_fp8 only: the result as the next fp8 GEMM's operand
 
 
 def _rowmajor(t, dtype, name):
-    if t.dtype != dtype:
+    if (t.dtype not in HALF) if dtype == HALF else (t.dtype != dtype):
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
     if t.dim() != 2 or t.stride(1) != 1:
         raise ValueError(f"{name}: expected a 2-D row-major view, got shape {tuple(t.shape)} "
                          f"strides {t.stride()}")
+
+
+def _sym16(name, *ts):
+    """The entry point for the 16-bit storage type of `ts` (None and f32 entries ignored): `name`
+    for bf16, `name`_f16 for IEEE half (include/lc_clip.h). The library reads raw pointers, so
+    every 16-bit operand and output of one call must share the type: checked here."""
+    kinds = {t.dtype for t in ts if t is not None and t.dtype in HALF}
+    if len(kinds) > 1:
+        raise TypeError(f"{name}: bf16 and float16 operands mixed in one call")
+    return name + "_f16" if kinds == {F16} else name
 
 
 SPLITK_TICKET_BYTES = 16384           # LC_SPLITK_TICKET_BYTES
@@ -40,10 +52,13 @@ def splitk_workspace(stream):
 
 
 def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
-    """out = epilogue(alpha * A @ B^T + bias); A [M,K] bf16, B [N,K] bf16. Large launches use
-    the current stream's split-K workspace for their tail round (lc_gemm_nt_ws)."""
-    _rowmajor(A, BF16, "A")
-    _rowmajor(B, BF16, "B")
+    """out = epilogue(alpha * A @ B^T + bias); A [M,K], B [N,K] bf16 (or both float16: the _f16
+    entry point; 16-bit outputs / side inputs then float16 too). Large launches use the current
+    stream's split-K workspace for their tail round (lc_gemm_nt_ws)."""
+    _rowmajor(A, HALF, "A")
+    _rowmajor(B, HALF, "B")
+    if B.dtype != A.dtype:
+        raise TypeError("gemm_nt: A and B must share the 16-bit type")
     M, K = A.shape
     N = B.shape[0]
     if B.shape[1] != K or out0.shape[0] != M or out0.shape[1] != N:
@@ -52,7 +67,7 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
         raise ValueError("gemm_nt bias must be a contiguous f32 vector of length N")
     st = stream_of(A)
     ws = splitk_workspace(torch.cuda.current_stream(A.device)) if M >= 4096 else None
-    call("lc_gemm_nt_ws", st, epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
+    call(_sym16("lc_gemm_nt_ws", A, out0, out1, aux), st, epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
          ptr(bias), float(alpha), ptr(out0), out0.stride(0), ptr(out1),
          out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
          ptr(ws), ws.numel() if ws is not None else 0)
@@ -143,8 +158,8 @@ def gemm_nt_fp8(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None, q_ou
 def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
     """C[N1,N2] += alpha * A[M,:N1]^T @ B[M,:N2] (C f32, N1 x N2 = C's shape); colsum[N1] +=
     colsum_scale * sum_m A[:, :N1]. A / B may be wider than N1 / N2 (zero padding to 64)."""
-    _rowmajor(A, BF16, "A")
-    _rowmajor(B, BF16, "B")
+    _rowmajor(A, HALF, "A")
+    _rowmajor(B, HALF, "B")
     _rowmajor(C, F32, "C")
     M = A.shape[0]
     N1, N2 = C.shape
@@ -157,7 +172,7 @@ def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
         raise ValueError("colsum must be f32 [N1]")
     # the launch stream's split-K workspace takes the two-stage partials (after its tickets)
     ws = splitk_workspace(torch.cuda.current_stream(A.device))
-    call("lc_gemm_tn_ws", stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
+    call(_sym16("lc_gemm_tn_ws", A, B), stream_of(A), M, N1, N2, ptr(A), A.stride(0), ptr(B), B.stride(0),
          float(alpha), ptr(C), C.stride(0), ptr(colsum), float(colsum_scale), ptr(ws), ws.numel())
     return C
 
@@ -166,7 +181,7 @@ def layernorm_fwd(x, weight, bias, y, mean=None, rstd=None, row_idx=None):
     _rowmajor(x, F32, "x")
     rows = y.shape[0]
     D = x.shape[1]
-    call("lc_layernorm_fwd", stream_of(x), rows, D, ptr(x), x.stride(0), ptr(row_idx),
+    call(_sym16("lc_layernorm_fwd", y), stream_of(x), rows, D, ptr(x), x.stride(0), ptr(row_idx),
          ptr(weight), ptr(bias), ptr(y), 1 if y.dtype == F32 else 0, y.stride(0), ptr(mean),
          ptr(rstd))
     return y
@@ -188,7 +203,7 @@ def layernorm_fwd_fp8(x, weight, bias, q, mean=None, rstd=None, y=None):
 def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_idx=None):
     rows = dy.shape[0]
     D = x.shape[1]
-    call("lc_layernorm_bwd", stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+    call(_sym16("lc_layernorm_bwd", dy, dx_bf16), stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
          dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
          ptr(dx_bf16), dx.stride(0), ptr(row_idx))
     return dx
@@ -261,7 +276,9 @@ def eot_rows(tokens, out):
 
 
 def attn_fwd(qkv, O, lse, n_seq, L, H, causal):
-    call("lc_attn_fwd", stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), O.stride(0),
+    if O.dtype != qkv.dtype or qkv.dtype not in HALF:
+        raise TypeError("attn_fwd: qkv and O must share the 16-bit type")
+    call(_sym16("lc_attn_fwd", qkv, O), stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), O.stride(0),
          ptr(lse), int(causal))
     return O
 
@@ -269,7 +286,9 @@ def attn_fwd(qkv, O, lse, n_seq, L, H, causal):
 def attn_bwd(qkv, O, dO, lse, dqkv, n_seq, L, H, causal):
     if O.stride(0) != dO.stride(0):
         raise ValueError("O and dO must share a row stride")
-    call("lc_attn_bwd", stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), ptr(dO),
+    if len({t.dtype for t in (qkv, O, dO, dqkv)}) != 1 or qkv.dtype not in HALF:
+        raise TypeError("attn_bwd: qkv, O, dO and dqkv must share the 16-bit type")
+    call(_sym16("lc_attn_bwd", qkv, O, dO, dqkv), stream_of(qkv), n_seq, L, H, ptr(qkv), qkv.stride(0), ptr(O), ptr(dO),
          O.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), int(causal))
     return dqkv
 
@@ -288,9 +307,9 @@ def attn_bwd_fp8(qkv, O, dO, lse, q, n_seq, L, H, causal):
 
 
 def cast_bf16(src, dst):
-    if src.dtype != F32 or not src.is_contiguous() or not dst.is_contiguous():
-        raise ValueError("cast_bf16 expects contiguous f32 -> bf16")
-    call("lc_cast_bf16", stream_of(src), src.numel(), ptr(src), ptr(dst))
+    if src.dtype != F32 or not src.is_contiguous() or not dst.is_contiguous() or dst.dtype not in HALF:
+        raise ValueError("cast_bf16 expects contiguous f32 -> bf16 / float16")
+    call(_sym16("lc_cast_bf16", dst), stream_of(src), src.numel(), ptr(src), ptr(dst))
     return dst
 
 
@@ -298,7 +317,7 @@ def merge_weight(W, A, B, scaling, out, outT=None):
     """out = bf16(W + scaling * B @ A); A/B None -> plain cast."""
     N, K = W.shape
     r = 0 if A is None else A.shape[0]
-    call("lc_merge_weight", stream_of(W), N, K, r, ptr(W), ptr(A), ptr(B), float(scaling),
+    call(_sym16("lc_merge_weight", out, outT), stream_of(W), N, K, r, ptr(W), ptr(A), ptr(B), float(scaling),
          ptr(out), ptr(outT))
     return out
 
@@ -314,8 +333,8 @@ def cast_weights(items):
         chunk = items[i:i + CAST_MAX]
         n = len(chunk)
         for W, out, outT in chunk:
-            if W.dtype != F32 or not W.is_contiguous() or out.dtype != BF16 or not out.is_contiguous():
-                raise ValueError("cast_weights: W must be contiguous f32, out contiguous bf16")
+            if W.dtype != F32 or not W.is_contiguous() or out.dtype not in HALF or not out.is_contiguous():
+                raise ValueError("cast_weights: W must be contiguous f32, out contiguous bf16 / float16")
             if out.shape != W.shape or (outT is not None and outT.shape != W.shape[::-1]):
                 raise ValueError("cast_weights: shape mismatch")
         ws = (ctypes.c_void_p * n)(*[ptr(W) for W, _, _ in chunk])
@@ -323,7 +342,8 @@ def cast_weights(items):
         Ks = (ctypes.c_int * n)(*[W.shape[1] for W, _, _ in chunk])
         outs = (ctypes.c_void_p * n)(*[ptr(o) for _, o, _ in chunk])
         outTs = (ctypes.c_void_p * n)(*[ptr(t) for _, _, t in chunk])
-        call("lc_cast_weights_bf16", stream_of(chunk[0][0]), n, ws, Ns, Ks, outs, outTs)
+        call(_sym16("lc_cast_weights_bf16", *[t for c in chunk for t in c[1:]]),
+             stream_of(chunk[0][0]), n, ws, Ns, Ks, outs, outTs)
 
 
 def merge_weights(items):
@@ -335,8 +355,8 @@ def merge_weights(items):
         chunk = items[i:i + CAST_MAX]
         n = len(chunk)
         for W, A, B, _, out, outT in chunk:
-            if W.dtype != F32 or not W.is_contiguous() or out.dtype != BF16 or not out.is_contiguous():
-                raise ValueError("merge_weights: W must be contiguous f32, out contiguous bf16")
+            if W.dtype != F32 or not W.is_contiguous() or out.dtype not in HALF or not out.is_contiguous():
+                raise ValueError("merge_weights: W must be contiguous f32, out contiguous bf16 / float16")
             if out.shape != W.shape or (outT is not None and (outT.shape != W.shape[::-1]
                                                               or not outT.is_contiguous())):
                 raise ValueError("merge_weights: shape mismatch")
@@ -355,24 +375,25 @@ def merge_weights(items):
         Ks = (ctypes.c_int * n)(*[c[0].shape[1] for c in chunk])
         outs = (P * n)(*[ptr(c[4]) for c in chunk])
         outTs = (P * n)(*[ptr(c[5]) for c in chunk])
-        call("lc_merge_weights_bf16", stream_of(chunk[0][0]), n, ws, As, Bs, rs, ss, Ns, Ks, outs,
+        call(_sym16("lc_merge_weights_bf16", *[t for c in chunk for t in c[4:]]),
+             stream_of(chunk[0][0]), n, ws, As, Bs, rs, ss, Ns, Ks, outs,
              outTs)
 
 
 def lora_grad(dY, X, A, B, scaling, dA, dB):
     M, N = dY.shape
     K = X.shape[1]
-    call("lc_lora_grad", stream_of(dY), M, N, K, A.shape[0], ptr(dY), dY.stride(0), ptr(X),
+    call(_sym16("lc_lora_grad", dY, X), stream_of(dY), M, N, K, A.shape[0], ptr(dY), dY.stride(0), ptr(X),
          X.stride(0), ptr(A), ptr(B), float(scaling), ptr(dA), ptr(dB))
 
 
 def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
     """dB [N,r] += s dY^T (X A^T), dA [r,K] += s (dY B)^T X in one pass over X and dY
     (lc_lora_grad_ws); a_pad [>=16, K] / bt_pad [>=16, N] bf16 with rows >= r zero."""
-    _rowmajor(dY, BF16, "dY")
-    _rowmajor(X, BF16, "X")
-    _rowmajor(a_pad, BF16, "a_pad")
-    _rowmajor(bt_pad, BF16, "bt_pad")
+    _rowmajor(dY, HALF, "dY")
+    _rowmajor(X, HALF, "X")
+    _rowmajor(a_pad, HALF, "a_pad")
+    _rowmajor(bt_pad, HALF, "bt_pad")
     M, N = dY.shape
     K = X.shape[1]
     if X.shape[0] != M or a_pad.shape[1] != K or bt_pad.shape[1] != N or a_pad.shape[0] < 16 \
@@ -385,14 +406,14 @@ def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
         if t.dtype != F32 or not t.is_contiguous() or not t.is_cuda:
             raise ValueError(f"lora_grad_1p: {name} must be a contiguous f32 device tensor")
     ws = splitk_workspace(torch.cuda.current_stream(dY.device))
-    call("lc_lora_grad_ws", stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
+    call(_sym16("lc_lora_grad_ws", dY, X, a_pad, bt_pad), stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
          ptr(a_pad), a_pad.stride(0), ptr(bt_pad), bt_pad.stride(0), float(scaling), ptr(dA),
          ptr(dB), ptr(ws), ws.numel())
 
 
 def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=None):
     M, D = z.shape
-    call("lc_adapter_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
+    call(_sym16("lc_adapter_fwd", z, Wd, Wu, h), stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
          ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
          ptr(resid), ptr(xout), xout.stride(0), ptr(h))
 
@@ -401,9 +422,9 @@ def adapter_ln_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, gamma, 
                    rstd, seed_dev=None):
     """adapter_fwd, then y = LayerNorm(xout) (bf16, statistics saved) in one launch."""
     M, D = z.shape
-    if y.dtype != BF16 or tuple(y.shape) != (M, D) or y.stride(1) != 1:
-        raise ValueError("adapter_ln_fwd: y must be a bf16 [M, D] row-major view")
-    call("lc_adapter_ln_fwd", stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
+    if y.dtype != z.dtype or tuple(y.shape) != (M, D) or y.stride(1) != 1:
+        raise ValueError("adapter_ln_fwd: y must be a [M, D] row-major view of z's 16-bit type")
+    call(_sym16("lc_adapter_ln_fwd", z, Wd, Wu, h, y), stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
          ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
          ptr(resid), ptr(xout), xout.stride(0), ptr(h), ptr(gamma), ptr(beta), ptr(y),
          y.stride(0), ptr(mean), ptr(rstd))
@@ -411,7 +432,7 @@ def adapter_ln_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, gamma, 
 
 def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
     M, D = gout.shape
-    call("lc_adapter_bwd", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
+    call(_sym16("lc_adapter_bwd", gout, h, WuT, WdT, dpre, dz), stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
          ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz),
          dz.stride(0) if dz is not None else D)
 
@@ -420,10 +441,10 @@ def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
     """dWu += scale gout^T h, dbu += scale colsum(gout), dWd += dpre^T z, dbd += colsum(dpre)."""
     M, D = gout.shape
     for t, name in ((gout, "gout"), (z, "z")):
-        _rowmajor(t, BF16, name)
+        _rowmajor(t, HALF, name)
     for t, name in ((h, "h"), (dpre, "dpre")):
-        if t.dtype != BF16 or not t.is_contiguous() or t.shape != (M, 64):
-            raise ValueError(f"{name} must be contiguous bf16 [M, 64]")
+        if t.dtype not in HALF or not t.is_contiguous() or t.shape != (M, 64):
+            raise ValueError(f"{name} must be contiguous 16-bit [M, 64]")
     if z.shape != (M, D) or dWu.shape != (D, 64) or dWd.shape != (64, D):
         raise ValueError("adapter_wgrad shape mismatch")
     for t in (dWu, dWd, dbu, dbd):
@@ -432,7 +453,7 @@ def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
     # two-stage reduction through the launch stream's split-K workspace (partials after its
     # ticket region; the stream orders every user of that buffer)
     ws = splitk_workspace(torch.cuda.current_stream(gout.device))
-    call("lc_adapter_wgrad_ws", stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
+    call(_sym16("lc_adapter_wgrad_ws", gout, h, z, dpre), stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
          z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd), ptr(ws),
          ws.numel())
 
@@ -490,3 +511,21 @@ def head_feat_grad(dlogits, sr, sc, other_n, self_n, norms, logit_scale, dF, dn_
     Co = other_n.shape[0]
     call("lc_head_feat_grad", stream_of(dlogits), R, Co, E, ptr(dlogits), sr, sc, ptr(other_n),
          ptr(self_n), ptr(norms), ptr(logit_scale), ptr(dn_ext), ptr(dF))
+
+
+def grad_pow2_normalize(x, scale, target_exp=10):
+    """x (contiguous f32) *= s in place, s = 2^(target_exp - floor(log2 max|x|)) on the device,
+    written to scale (f32 [1]): the IEEE-half text tower's per-call loss scaling."""
+    if x.dtype != F32 or not x.is_contiguous() or scale.dtype != F32 or scale.numel() < 1:
+        raise ValueError("grad_pow2_normalize: contiguous f32 x and an f32 scale slot")
+    call("lc_grad_pow2_normalize", stream_of(x), x.numel(), ptr(x), ptr(scale), int(target_exp))
+    return x
+
+
+def add_unscaled(y, x, scale):
+    """y += x / scale[0] (contiguous f32, same size)."""
+    if (y.dtype != F32 or x.dtype != F32 or not y.is_contiguous() or not x.is_contiguous()
+            or y.numel() != x.numel()):
+        raise ValueError("add_unscaled: contiguous f32 tensors of one size")
+    call("lc_add_unscaled", stream_of(y), y.numel(), ptr(y), ptr(x), ptr(scale))
+    return y

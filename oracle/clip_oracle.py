@@ -45,7 +45,12 @@ module by tests/golden/make_golden.py.
 Rounding hook. Every function takes ``rt`` (default identity). With ``rt = round_bf16`` the
 oracle rounds exactly where the MI355X path rounds (GEMM/attention operands and the bf16
 activations it stores), so the HIP forward can be checked at a tight tolerance; with the
-identity it is the plain fp32 reference algorithm.
+identity it is the plain fp32 reference algorithm. ``round_bf16`` / ``round_f16`` are straight-through
+(forward rounding only); ``round_bf16_fwd_bwd`` / ``round_f16_fwd_bwd`` (``Rounding``) also round
+where the HIP backward stores 16-bit gradients, so the GPU's gradients can be checked against an
+oracle that makes the same roundings (its distance then measures implementation error, not
+emulation gaps). The MI355X path stores the image tower in bf16 and the text tower in IEEE half
+(``rt_text``).
 """
 from __future__ import annotations
 
@@ -67,6 +72,149 @@ def round_bf16(x):
     """Round-to-nearest-even fp32 -> bf16 -> fp32 (value-preserving forward, STE backward)."""
     r = x.detach().to(torch.bfloat16).to(x.dtype)
     return x + (r - x).detach()
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def _hf(x):
+    return x.to(torch.float16).to(x.dtype)
+
+
+def round_f16(x):
+    """Round-to-nearest-even fp32 -> IEEE half -> fp32 (value-preserving forward, STE backward):
+    the MI355X text tower's storage (lcclip AdapterCLIP text_precision='fp16', the reference's
+    autocast dtype, methods/adapter_clip.py:87)."""
+    r = _hf(x.detach())
+    return x + (r - x).detach()
+
+
+class _GradRound(torch.autograd.Function):
+    """Identity forward; the incoming gradient rounded by `rnd`: a point where the HIP backward
+    stores a 16-bit gradient that the next GEMM reads."""
+
+    @staticmethod
+    def forward(ctx, x, rnd):
+        ctx.rnd = rnd
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.rnd(g), None
+
+
+class _GradScaleSet(torch.autograd.Function):
+    """Identity forward; in backward sets the hook's gradient scale from the incoming gradient,
+    s = 2^(10 - floor(log2 max|g|)) (the IEEE-half text tower's per-call loss scale,
+    ops.grad_pow2_normalize / head.hip), before any rounding inside the tower runs."""
+
+    @staticmethod
+    def forward(ctx, x, hook):
+        ctx.hook = hook
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        a = g.abs().max().item()
+        ctx.hook.gs = 2.0 ** (10 - math.floor(math.log2(a))) if 0 < a < float("inf") else 1.0
+        return g, None
+
+
+class _QuickGeluRound(torch.autograd.Function):
+    """quick_gelu whose backward multiplies by QuickGELU'(pre) rounded to the storage type: the
+    c_fc epilogue stores the derivative (EPI_GELU_D, gemm.hip) and the c_proj input-gradient
+    epilogue multiplies its f32 accumulator by it (EPI_MUL); the product is rounded where the
+    caller puts the gradient rounding."""
+
+    @staticmethod
+    def forward(ctx, x, rnd):
+        ctx.save_for_backward(x)
+        ctx.rnd = rnd
+        return quick_gelu(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        sg = torch.sigmoid(1.702 * x)
+        return g * ctx.rnd(sg + 1.702 * x * sg * (1 - sg)), None
+
+
+class _AttnCoreRound(torch.autograd.Function):
+    """attention_core's rounded forward, with the backward of the HIP kernel
+    (attention.hip:456-806) on the 16-bit q, k, v, O, dO: P = exp(S - lse) recomputed in f32,
+    D = rowsum(dO O), dS = P (dO V^T - D); dV = P_16^T dO, dK = scale dS_16^T Q,
+    dQ = scale dS_16 K, each stored 16-bit. rnd rounds values (P), grnd gradients (dO, dS and
+    the dq|dk|dv store; the IEEE-half tower's carry its loss scale)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal, rnd, grnd):
+        s = (q @ k.transpose(-1, -2)) * scale
+        if causal:
+            L = s.shape[-1]
+            s = s + torch.full((L, L), float("-inf")).triu_(1)
+        m = s.amax(dim=-1, keepdim=True)
+        pe = torch.exp(s - m)
+        l = pe.sum(dim=-1, keepdim=True)
+        o = rnd((rnd(pe) @ v) / l)
+        ctx.save_for_backward(q, k, v, o, m + torch.log(l))
+        ctx.scale, ctx.causal, ctx.rnd, ctx.grnd = scale, causal, rnd, grnd
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        scale, rnd, grnd = ctx.scale, ctx.rnd, ctx.grnd
+        do = grnd(do)
+        s = (q @ k.transpose(-1, -2)) * scale
+        if ctx.causal:
+            L = s.shape[-1]
+            s = s + torch.full((L, L), float("-inf")).triu_(1)
+        p = torch.exp(s - lse)
+        d = (do * o).sum(dim=-1, keepdim=True)
+        ds = p * (do @ v.transpose(-1, -2) - d)
+        dsb = grnd(ds)
+        dq = grnd(scale * (dsb @ k))
+        dk = grnd(scale * (dsb.transpose(-1, -2) @ q))
+        dv = grnd(rnd(p).transpose(-1, -2) @ do)
+        return dq, dk, dv, None, None, None, None
+
+
+class Rounding:
+    """A rounding hook for the oracle's ``rt`` argument: called on a tensor it rounds the value
+    to the storage type (straight-through gradient), like ``round_bf16``. With backward=True it
+    also carries the HIP backward's roundings, read by the functions that take ``rt``:
+    ``bwd`` (the gradient rounding at each 16-bit gradient store: the features' gradient, dY
+    into each input-gradient GEMM, dpre, dz, da, dh, dO), ``gelu`` (the stored QuickGELU') and
+    ``attn`` (the attention backward above); kind 'f16' adds ``top`` (the per-call gradient
+    scale, set at the tower output and applied inside every gradient rounding)."""
+
+    def __init__(self, kind, backward=False):
+        self.kind = kind
+        self._rnd = {"bf16": _bf, "f16": _hf}[kind]
+        self.gs = 1.0
+        if backward:
+            self.bwd = lambda x: _GradRound.apply(x, self._grnd)
+            self.gelu = lambda x: _QuickGeluRound.apply(x, self._rnd)
+            self.attn = lambda q, k, v, scale, causal: _AttnCoreRound.apply(
+                q, k, v, scale, causal, self._rnd, self._grnd)
+            if kind == "f16":
+                self.top = lambda x: _GradScaleSet.apply(x, self)
+
+    def __call__(self, x):
+        r = self._rnd(x.detach())
+        return x + (r - x).detach()
+
+    def _grnd(self, g):
+        s = self.gs
+        return self._rnd(g * s) / s if s != 1.0 else self._rnd(g)
+
+
+# forward + backward roundings of the MI355X path: the image tower (bf16) and the text tower
+# (IEEE half, text_precision='fp16'); the straight-through round_bf16 / round_f16 round the
+# forward only, so their gradients miss the backward's roundings (DESIGN.md §2)
+round_bf16_fwd_bwd = Rounding("bf16", backward=True)
+round_f16_fwd_bwd = Rounding("f16", backward=True)
 
 
 @dataclass(frozen=True)
@@ -269,6 +417,8 @@ def attention_core(q, k, v, scale, causal, rt=identity):
     from bf16 q,k; P = exp(S - max) rounded to bf16 for the PV product; the row sum l is taken
     from the unrounded fp32 exponentials; O = (P_bf16 @ V) / l, rounded to bf16."""
     q, k, v = rt(q), rt(k), rt(v)
+    if getattr(rt, "attn", None) is not None:
+        return rt.attn(q, k, v, scale, causal)
     s = (q @ k.transpose(-1, -2)) * scale
     if causal:
         L = s.shape[-1]
@@ -311,8 +461,9 @@ def adapter(z, p, pre, scale=0.1, dropout_mask=None, rt=identity):
     """adapter.py:53-72 with adapter_layernorm_option='none' (model.py:436):
     out = z + scale * up(dropout(relu(down(z)))). ``dropout_mask`` (already divided by keep
     probability) replaces F.dropout when given; None means eval / p = 0."""
-    d = torch.relu(linear(z, p[pre + "adaptmlp.down_proj.weight"],
-                          p[pre + "adaptmlp.down_proj.bias"], rt))
+    gq = getattr(rt, "bwd", identity)  # dpre stored as bf16 (peft.hip adapter backward)
+    d = torch.relu(gq(linear(z, p[pre + "adaptmlp.down_proj.weight"],
+                             p[pre + "adaptmlp.down_proj.bias"], rt)))
     if dropout_mask is not None:
         d = d * dropout_mask
     u = linear(d, p[pre + "adaptmlp.up_proj.weight"], p[pre + "adaptmlp.up_proj.bias"], rt)
@@ -323,22 +474,28 @@ def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, ma
     """ResidualAttentionBlock{,_LoRA} forward (model.py:233-236) and _Adapter forward
     (model.py:439-442; one adapter module reused for both sub-blocks, Q6). x is the fp32
     residual stream [N, L, D]."""
-    h = rt(layer_norm(x, p[pre + "ln_1.weight"], p[pre + "ln_1.bias"]))
+    # gq: the backward's bf16 gradient stores (rt.bwd; identity for the fp32 oracle and the
+    # straight-through round_bf16): the residual stream's gradient stays f32 and each sub-block
+    # reads its bf16 copy (dx_midb / the layer's output pair, engine.py BlockStack.backward);
+    # dz, dO, da (c_proj dX x QuickGELU'), dh (c_fc dX, QKV dX) are bf16
+    gq = getattr(rt, "bwd", identity)
+    gelu = getattr(rt, "gelu", quick_gelu)
+    h = gq(rt(layer_norm(x, p[pre + "ln_1.weight"], p[pre + "ln_1.bias"])))
     a = mha(h, p, pre, n_head, causal, lora_scaling if variant == "lora" else None, rt)
     if variant == "adapter":
         m0 = None if masks is None else masks[0]
-        x = x + adapter(rt(a), p, pre, dropout_mask=m0, rt=rt)
+        x = x + gq(adapter(gq(rt(a)), p, pre, dropout_mask=m0, rt=rt))
     else:
-        x = x + a
-    h2 = rt(layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"]))
-    f = rt(quick_gelu(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt,
-                             fp8=True)))
+        x = x + gq(a)
+    h2 = gq(rt(layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"])))
+    f = rt(gelu(gq(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt,
+                          fp8=True))))
     m = linear(f, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"], rt, fp8=True)
     if variant == "adapter":
         m1 = None if masks is None else masks[1]
-        x = x + adapter(rt(m), p, pre, dropout_mask=m1, rt=rt)
+        x = x + gq(adapter(gq(rt(m)), p, pre, dropout_mask=m1, rt=rt))
     else:
-        x = x + m
+        x = x + gq(m)
     return x
 
 
@@ -366,8 +523,11 @@ def encode_image(img, p, cfg: ClipConfig, method="vanilla", peft_encoder="none",
     for i, pre in enumerate(vis):
         x = block(x, p, pre, cfg.vision_heads, False, variant, rt=rt,
                   masks=None if masks is None else masks[i])
-    x = rt(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))  # :783
-    return linear(x, p["visual.proj"].t(), None, rt)                            # :785
+    tail = getattr(rt, "tail", rt)  # rounding of ln_post's output and the projection GEMM
+    x = tail(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))  # :783
+    # the feature gradient is cast to 16 bits before the projection's backward GEMM
+    return getattr(rt, "top", identity)(
+        getattr(rt, "bwd", identity)(linear(x, p["visual.proj"].t(), None, tail)))  # :785
 
 
 def encode_text(tokens, p, cfg: ClipConfig, method="vanilla", peft_encoder="none", rt=identity,
@@ -384,8 +544,10 @@ def encode_text(tokens, p, cfg: ClipConfig, method="vanilla", peft_encoder="none
                   masks=None if masks is None else masks[i])
     eot = tokens.argmax(dim=-1)
     x = x[torch.arange(C), eot]
-    x = rt(layer_norm(x, p["ln_final.weight"], p["ln_final.bias"]))
-    return linear(x, p["text_projection"].t(), None, rt)
+    tail = getattr(rt, "tail", rt)  # rounding of ln_final's output and the projection GEMM
+    x = tail(layer_norm(x, p["ln_final.weight"], p["ln_final.bias"]))
+    return getattr(rt, "top", identity)(
+        getattr(rt, "bwd", identity)(linear(x, p["text_projection"].t(), None, tail)))
 
 
 def clip_logits(img_f, txt_f, logit_scale):
@@ -396,10 +558,12 @@ def clip_logits(img_f, txt_f, logit_scale):
 
 
 def adapter_clip_forward(img, tokens, p, cfg, method, peft_encoder, rt=identity,
-                         img_masks=None, txt_masks=None):
-    """AdapterCLIP.forward, models/adapter_clip.py:94-100 -> (probs, img_f, txt_f)."""
+                         img_masks=None, txt_masks=None, rt_text=None):
+    """AdapterCLIP.forward, models/adapter_clip.py:94-100 -> (probs, img_f, txt_f). rt_text:
+    the text tower's rounding hook when it differs from the image tower's (default rt)."""
     fi = encode_image(img, p, cfg, method, peft_encoder, rt, img_masks)
-    ft = encode_text(tokens, p, cfg, method, peft_encoder, rt, txt_masks)
+    ft = encode_text(tokens, p, cfg, method, peft_encoder, rt if rt_text is None else rt_text,
+                     txt_masks)
     logits, i, t = clip_logits(fi, ft, p["logit_scale"])
     return logits.softmax(dim=-1), i, t
 
@@ -430,12 +594,14 @@ def adamw_step(params, grads, state, lr=5e-4, betas=(0.9, 0.999), eps=1e-8, wd=1
     return out
 
 
-def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-4, state=None):
+def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-4, state=None,
+               rt_text=None):
     """methods/adapter_clip.py:86-96 at p=0 dropout: fwd -> CE(probs) -> bwd -> AdamW.
     state: the AdamW state carried across steps (None: a fresh optimizer).
     Returns (loss, probs, img_f, txt_f, grads, new_params)."""
     leaves = {n: t.detach().clone().requires_grad_(is_trainable(n)) for n, t in p.items()}
-    probs, fi, ft = adapter_clip_forward(img, tokens, leaves, cfg, method, peft_encoder, rt)
+    probs, fi, ft = adapter_clip_forward(img, tokens, leaves, cfg, method, peft_encoder, rt,
+                                         rt_text=rt_text)
     loss = loss_on_probs(probs, y)
     train = {n: t for n, t in leaves.items() if t.requires_grad}
     if not train:  # vanilla blocks: nothing is trainable (the freeze filter leaves no params)
@@ -447,7 +613,7 @@ def train_step(img, tokens, y, p, cfg, method, peft_encoder, rt=identity, lr=5e-
 
 
 def online_loop(task_batches, images, labels, class_tokens, p, cfg, method="adapter",
-                peft_encoder="both", online_iter=3, lr=5e-4, rt=identity):
+                peft_encoder="both", online_iter=3, lr=5e-4, rt=identity, rt_text=None):
     """The online loop of methods/_trainer.py:320-357 + methods/adapter_clip.py:34-107, restated
     for the trajectory parity test (replay memory off, visible_classes='batch', p = 0 dropout,
     inputs already transformed). task_batches: per task, the list of sample-index lists the
@@ -476,7 +642,7 @@ def online_loop(task_batches, images, labels, class_tokens, p, cfg, method="adap
                 yi = torch.tensor([batch_list.index(y) for y in ys], dtype=torch.long)
                 tok = class_tokens[torch.tensor(batch_list)]
                 loss, _, _, _, _, new = train_step(images[b], tok, yi, params, cfg, method,
-                                                   peft_encoder, rt, lr, state)
+                                                   peft_encoder, rt, lr, state, rt_text=rt_text)
                 params.update(new)
                 out.append((loss, {n: t.clone() for n, t in new.items()}))
     return out

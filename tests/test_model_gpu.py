@@ -180,7 +180,8 @@ def test_vit_b16_full_shapes_vs_oracle(dev, method):
     tok = o.synthetic_tokens(4, 77, seed=1)
     with torch.no_grad():
         p32, i32, t32 = o.adapter_clip_forward(img, tok, sd, cfg, method, "both")
-        p16, i16, t16 = o.adapter_clip_forward(img, tok, sd, cfg, method, "both", rt=o.round_bf16)
+        p16, i16, t16 = o.adapter_clip_forward(img, tok, sd, cfg, method, "both", rt=o.round_bf16,
+                                               rt_text=o.round_f16)
     w = make_wrapper(sd, method, "both", dev)
     with torch.no_grad():
         probs, fi, ft = w(img.to(dev), tok.to(dev))
@@ -221,7 +222,11 @@ def _step_vs_oracle(dev, method, B, C, seed, tag):
     tok = o.synthetic_tokens(C, 77, seed=seed + 2)
     y = torch.arange(B) % C
     loss32, p32, i32, t32, g32, _ = o.train_step(img, tok, y, sd, cfg, method, "both")
-    g16 = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16)[4]
+    g16 = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16,
+                       rt_text=o.round_f16)[4]
+    # the oracle that also rounds where the HIP backward stores bf16 gradients
+    gfb = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16_fwd_bwd,
+                       rt_text=o.round_f16_fwd_bwd)[4]
     w = make_wrapper(sd, method, "both", dev)
     with torch.no_grad():
         _, fi, ft = w(img.to(dev), tok.to(dev))
@@ -242,12 +247,19 @@ def _step_vs_oracle(dev, method, B, C, seed, tag):
     flat, flat_o = rel(cat(gg), cat(g32)), rel(cat(g16), cat(g32))
     flat_b = rel(cat(gg), cat(g16))  # vs the bf16-rounding oracle: the implementation's fidelity
     cos_b = {n: cs(gg[n], g16[n]) for n in g32}
+    flat_fb = rel(cat(gg), cat(gfb))
+    cos_fb = {n: cs(gg[n], gfb[n]) for n in g32}
+    worst_fb = min(cos_fb, key=cos_fb.get)
     m = dict(probs_abs_vs_fp32=(probs.cpu() - p32).abs().max().item(),
              loss_abs=abs(loss.item() - loss32.item()), grad_flat_rel_vs_fp32=flat,
              grad_rel_max_vs_fp32=max(e32.values()), grad_cos_min=min(cos.values()),
              oracle_bf16_grad_flat_rel=flat_o, oracle_bf16_grad_rel_max=max(eo.values()),
              oracle_bf16_grad_cos_min=min(cos_o.values()), n_grads=len(e32),
              grad_flat_rel_vs_bf16_oracle=flat_b, grad_cos_min_vs_bf16_oracle=min(cos_b.values()),
+             grad_flat_rel_vs_fwdbwd_oracle=flat_fb,
+             grad_cos_min_vs_fwdbwd_oracle=cos_fb[worst_fb], worst_vs_fwdbwd=worst_fb,
+             fwdbwd_oracle_flat_rel_vs_fp32=rel(cat(gfb), cat(g32)),
+             fwdbwd_oracle_cos_min_vs_fp32=min(cs(gfb[n], g32[n]) for n in g32),
              **logit_metrics(ls * fi.cpu() @ ft.cpu().t(), ls * i32 @ t32.t(), None, ls))
     record(test=tag, method=method, B=B, C=C, **m)
     assert m["probs_abs_vs_fp32"] < 1e-2 and m["loss_abs"] < 1e-2, m
@@ -299,7 +311,7 @@ def test_lora_config4_shape_vs_oracle(dev):
     with torch.no_grad():
         _, i32, t32 = o.adapter_clip_forward(img[pick], tok, sd, cfg, "lora", "both")
         _, i16, t16 = o.adapter_clip_forward(img[pick], tok, sd, cfg, "lora", "both",
-                                             rt=o.round_bf16)
+                                             rt=o.round_bf16, rt_text=o.round_f16)
     ls = math.exp(sd["logit_scale"].item())
     lg = ls * fi[pick] @ ft.t()
     # The north-star bounds vs fp32 (RMS < 1e-3, max < 2e-3) as everywhere. Against the
@@ -374,7 +386,7 @@ def test_multi_step_staging_tracks_updates(golden, dev, method):
     moved = max((now[n] - sd[n]).abs().max().item() for n in now if o.is_trainable(n))
     assert moved > 1e-2  # the PEFT weights did move
     ref, _, _ = o.adapter_clip_forward(img.cpu(), tok.cpu(), now, o.TINY, method, "both",
-                                       rt=o.round_bf16)
+                                       rt=o.round_bf16, rt_text=o.round_f16)
     err = (probs.cpu() - ref).abs().max().item()
     record(test="multi_step_staging", method=method, probs_abs_vs_bf16_oracle=err, moved=moved)
     assert err < 4e-3

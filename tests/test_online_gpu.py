@@ -84,7 +84,7 @@ def test_online_loop_trajectory_vs_oracle(dev):
     batches = [[stream.task_indices(t)] for t in range(2)]
     assert all(len(b[0]) == 4 for b in batches)
     ref = o.online_loop(batches, imgs, labels, class_tokens, sd, cfg, online_iter=3, lr=lr,
-                        rt=o.round_bf16)
+                        rt=o.round_bf16, rt_text=o.round_f16)
     assert len(ref) == 6
     prev_ref = flat(sd, order)
     met = []
@@ -114,7 +114,7 @@ def test_online_loop_detects_missing_optimizer_reset(dev):
     _, _, snaps, order, _ = run_gpu(dev, lr, reset=False)
     batches = [[stream.task_indices(t)] for t in range(2)]
     ref = o.online_loop(batches, imgs, labels, class_tokens, sd, cfg, online_iter=3, lr=lr,
-                        rt=o.round_bf16)
+                        rt=o.round_bf16, rt_text=o.round_f16)
     p3 = flat({**{n: sd[n] for n in order}, **ref[2][1]}, order)
     p4 = flat({**{n: sd[n] for n in order}, **ref[3][1]}, order)
     d_ref = p4 - p3
