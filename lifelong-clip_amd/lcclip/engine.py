@@ -775,6 +775,9 @@ class ImageTower:
     def forward(self, img, save: bool, training: bool = False, prompts=None):
         """img -> (features f32 [n, E], ctx). prompts: {layer: f32 [n, P, D]} appended before
         that layer (prompt tuning, models/mvp_clip.py:158-175)."""
+        if self.stack.dt != BF16:
+            raise ValueError("the image tower runs on bf16 storage (BASELINE config 2); float16 "
+                             "storage is the text tower's")
         if (self.FUSE_EMBED and not prompts and self.stack.precision == "bf16"
                 and self.visual.width in (512, 768, 1024)):
             x0, n, L, first = self.embed_ln1(img)

@@ -168,7 +168,9 @@ def test_adapter_f16(ops, dev, D, M, keep):
     y2 = torch.empty(M, D, device=dev, dtype=HF)
     m2, r2 = torch.empty(M, device=dev), torch.empty(M, device=dev)
     ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, keep, 1234, x, xo2, h2, gam, bet, y2, m2, r2)
-    assert torch.equal(h2, h) and rel(xo2, xo) < 1e-6
+    # the fused walker splits the down projection's K across two waves: another summation
+    # order than the GEMM path, so h agrees to half rounding, not bit for bit
+    assert rel(h2, h) < TOL16 and rel(xo2, xo) < 1e-5
     y_ref = torch.nn.functional.layer_norm(xo, (D,), gam, bet, 1e-5)
     assert rel(y2, y_ref) < TOL16
     # backward: dpre = (h > 0) 0.1 (g Wu) / keep, dz = g + dpre Wd
@@ -217,8 +219,8 @@ def test_weight_staging_f16(ops, dev):
     items = [(torch.randn(64, 512, device=dev), torch.empty(64, 512, device=dev, dtype=HF),
               torch.empty(512, 64, device=dev, dtype=HF)) for _ in range(3)]
     ops.cast_weights(items)
-    for W, o_, oT in items:
-        assert torch.equal(o_, W.to(HF)) and torch.equal(oT, W.t().to(HF))
+    for Wi, o_, oT in items:
+        assert torch.equal(o_, Wi.to(HF)) and torch.equal(oT, Wi.t().to(HF))
     ops.merge_weights([(W, A, B, 0.25, out, outT)])
     assert rel(out, ref) < TOL16
     src = torch.randn(1000, device=dev)

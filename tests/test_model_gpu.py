@@ -67,7 +67,12 @@ def test_golden_trainer_step(golden, dev, method):
     y = torch.from_numpy(d["labels"]).to(dev)
     tr = OnlineTrainer(w)
     loss, probs = tr.forward_backward(img, y, tok)
-    e16 = (probs - torch.from_numpy(d[f"{method}/bf16/probs"]).to(dev)).abs().max().item()
+    # the rounding oracle of the path: bf16 image tower, IEEE-half text tower (the fixture's
+    # bf16/probs rounds both towers to bf16)
+    with torch.no_grad():
+        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), sd, o.TINY, method, "both",
+                                     rt=o.round_bf16, rt_text=o.round_f16)[0]
+    e16 = (probs.cpu() - p16).abs().max().item()
     e32 = (probs - torch.from_numpy(d[f"{method}/probs"]).to(dev)).abs().max().item()
     eloss = abs(loss.item() - float(d[f"{method}/loss"][0]))
     named = dict(w.model.named_parameters())
@@ -125,7 +130,10 @@ def test_module_path_matches_fused_trainer(golden, dev, method):
     probs, fi, ft = w(img)
     loss = torch.nn.functional.cross_entropy(probs, y)
     loss.backward()
-    assert (probs - torch.from_numpy(d[f"{method}/bf16/probs"]).to(dev)).abs().max() < 4e-3
+    with torch.no_grad():
+        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), sd, o.TINY, method, "both",
+                                     rt=o.round_bf16, rt_text=o.round_f16)[0]
+    assert (probs.detach().cpu() - p16).abs().max() < 4e-3
     assert rel(fi, torch.from_numpy(d[f"{method}/bf16/img_f"]) /
                torch.from_numpy(d[f"{method}/bf16/img_f"]).norm(dim=-1, keepdim=True)) < 5e-3
     w2 = make_wrapper(sd, method, "both", dev)
