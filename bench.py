@@ -333,6 +333,8 @@ def main():
                          "(exercises the collective path; launch through torch.distributed.run)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a HIP graph (1 GPU; measured equal to eager at B=256)")
+    ap.add_argument("--text-precision", default="fp16", choices=["fp16", "bf16"],
+                    help="the text tower's 16-bit storage (AdapterCLIP text_precision)")
     ap.add_argument("--gemm-tile", type=int, default=0,
                     help="A/B knob: lc_gemm_set_tile value for every GEMM (0 = automatic)")
     args = ap.parse_args()
@@ -361,7 +363,8 @@ def main():
             raise SystemExit(f"--gemm-tile {args.gemm_tile} rejected")
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
-    model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev)
+    model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev,
+                        text_precision=args.text_precision)
     trainer = OnlineTrainer(model, distributed=dp,
                             shard_text=os.environ.get("LCCLIP_DP_NOSHARD") != "1",
                             overlap_text=os.environ.get("LCCLIP_OVERLAP_TEXT", "1") != "0",
@@ -428,6 +431,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
+            "text_tower_dtype": {"fp16": "f16", "bf16": "bf16"}[args.text_precision],
             "data": "synthetic (random-init ViT-B/16 CLIP weights, U[0,1) images normalised with "
                     "CIFAR-100 stats, random prompt token ids)",
             "config": {"workload": f"{args.method}_clip ViT-B/16 both towers, online_train step "

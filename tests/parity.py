@@ -11,12 +11,19 @@ from fp32 in max cosine units and 1-4 % in per-logit relative terms at these sha
 The bounds, on d = (logits - logits_ref) / s over the whole B x C matrix:
   rms(d) vs the fp32 oracle          < 1e-3   (the north-star bound, as an RMS over the logits;
                                                TINY configs: see check_logits)
-  max|d| vs the fp32 oracle          < 2e-3   (bf16 compute: the bf16-rounding oracle alone, with
+  max|d| vs the fp32 oracle          < 1e-3   (the north-star bound as a max, ViT-B/16 shapes
+                                               with the IEEE-half text tower: measured 6.2e-4 ..
+                                               7.5e-4 on the four train-step tests, r5; with a
+                                               bf16 text tower the bf16-rounding oracle alone is
+                                               already 1.04e-3 there, tools/logit_conditioning.py)
+                                     < 2e-3   (towers that keep a bf16 text tower — MaPLe — and the
+                                               TINY configs: the bf16-rounding oracle alone, with
                                                no kernel error, reaches 1.5e-3 on TINY MaPLe)
-  max|d| vs the bf16-rounding oracle < 8e-4   (same rounding points as the kernels; what remains is
+  max|d| vs the rounding oracle      < 8e-4   (same rounding points as the kernels; what remains is
                                                accumulation order; measured 1.8e-4 .. 6.3e-4)
 """
 NORTH_STAR_RMS = 1e-3
+NORTH_STAR_MAX = 1e-3
 MAX_VS_FP32 = 2e-3
 MAX_VS_BF16 = 8e-4
 GRAD_REL = 4e-2  # PEFT gradients vs fp32 oracle, rel-norm per tensor (measured max 3.0e-2)
@@ -37,16 +44,17 @@ def logit_metrics(logits, ref32, ref16, scale):
     return met
 
 
-def check_logits(met, tiny=False):
+def check_logits(met, tiny=False, bf16_text=False):
     """ViT-B/16 shapes: the bounds above. TINY configs (64-wide synthetic towers, not the north
     star's model): there the bf16-rounding oracle alone — the kernels' rounding points with no
     kernel error — already sits at 0.96e-3 RMS (1.52e-3 max) from fp32 on TINY MaPLe (the kernels:
     1.06e-3 RMS), so the RMS bound is max(1e-3, 1.25 x that oracle distance + 1e-4): the kernels
-    may not add more than a quarter to the error bf16 storage itself implies."""
+    may not add more than a quarter to the error bf16 storage itself implies. bf16_text: a
+    model whose text tower also stores bf16 (MaPLe: max bound 2e-3 instead of 1e-3)."""
     rms_bound = NORTH_STAR_RMS
     if tiny and "oracle_bf16_cos_rms_vs_fp32" in met:
         rms_bound = max(NORTH_STAR_RMS, 1.25 * met["oracle_bf16_cos_rms_vs_fp32"] + 1e-4)
     assert met["cos_rms_vs_fp32"] < rms_bound, met
-    assert met["cos_err_vs_fp32"] < MAX_VS_FP32, met
+    assert met["cos_err_vs_fp32"] < (MAX_VS_FP32 if tiny or bf16_text else NORTH_STAR_MAX), met
     if "cos_err_vs_bf16" in met:
         assert met["cos_err_vs_bf16"] < MAX_VS_BF16, met

@@ -50,6 +50,11 @@ def make_wrapper(sd, method, peft, dev, dropout=0.0):
     return set_adapter_dropout(w, dropout)
 
 
+def method_sd(sd, method):
+    """The golden state dict holds every method's parameters: the ones `method` builds."""
+    return {k: sd[k] for k in o.param_shapes(o.TINY, method, "both")}
+
+
 @pytest.fixture(scope="module")
 def golden():
     d = np.load(GOLDEN)
@@ -70,8 +75,8 @@ def test_golden_trainer_step(golden, dev, method):
     # the rounding oracle of the path: bf16 image tower, IEEE-half text tower (the fixture's
     # bf16/probs rounds both towers to bf16)
     with torch.no_grad():
-        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), sd, o.TINY, method, "both",
-                                     rt=o.round_bf16, rt_text=o.round_f16)[0]
+        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), method_sd(sd, method), o.TINY, method,
+                                     "both", rt=o.round_bf16, rt_text=o.round_f16)[0]
     e16 = (probs.cpu() - p16).abs().max().item()
     e32 = (probs - torch.from_numpy(d[f"{method}/probs"]).to(dev)).abs().max().item()
     eloss = abs(loss.item() - float(d[f"{method}/loss"][0]))
@@ -131,8 +136,8 @@ def test_module_path_matches_fused_trainer(golden, dev, method):
     loss = torch.nn.functional.cross_entropy(probs, y)
     loss.backward()
     with torch.no_grad():
-        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), sd, o.TINY, method, "both",
-                                     rt=o.round_bf16, rt_text=o.round_f16)[0]
+        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), method_sd(sd, method), o.TINY, method,
+                                     "both", rt=o.round_bf16, rt_text=o.round_f16)[0]
     assert (probs.detach().cpu() - p16).abs().max() < 4e-3
     assert rel(fi, torch.from_numpy(d[f"{method}/bf16/img_f"]) /
                torch.from_numpy(d[f"{method}/bf16/img_f"]).norm(dim=-1, keepdim=True)) < 5e-3
@@ -207,22 +212,19 @@ def test_vit_b16_full_shapes_vs_oracle(dev, method):
     check_logits(m)  # north star: logits within 1e-3 (cosine units, RMS)
 
 
-def _step_vs_oracle(dev, method, B, C, seed, tag):
+def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None):
     """One fused trainer fwd + CE-on-probs + bwd at ViT-B/16 shapes vs the oracle's train_step
     on the same weights: probs, loss, logits (tests/parity.py bounds) and every PEFT gradient.
     Gradients vs the fp32 oracle: the whole flat PEFT gradient rel-norm < GRAD_REL and every
-    tensor's direction cosine >= 0.99 — or, where bf16 rounding alone moves them further (the
-    bf16-rounding oracle's own distance from fp32: flat rel f_o, per-tensor cosine c_o), flat rel <
-    1.25 f_o + 1e-2 and cosine >= c_o - 0.03. That happens at large C: with near-uniform
-    probabilities over 100 classes the loss gradient is small, the per-row terms of the adapter
-    down-projection gradients (dW_down = sum_rows dpre z^T) mostly cancel, and the bf16-rounding
-    oracle is up to 25 % (cosine 0.967) from fp32 on them; the GPU's backward also rounds dpre and
-    dY to bf16 (as the reference's fp16 autocast does), so it sits a little further.
-    It also fires at config 2's own shape (B = 32, C = 10): measured 7.2e-2 flat vs fp32, worst
-    tensor rel 0.209, min cosine 0.981, where the bf16-rounding oracle is 7.2e-2 / 0.215 / 0.980
-    (profiles/r03/s6/parity_metrics.jsonl). tools/conditioning.py (profiles/r04/) locates it:
-    at B = 32 / C = 10 the image tower's bf16 forward alone is 5.4e-2 from fp32 (text tower
-    exact), at C = 100 the text tower's (1.4e-2 with it exact) — DESIGN.md §2."""
+    tensor's direction cosine >= 0.99, with no oracle-relative escape (the IEEE-half text tower
+    brought C = 100 from 4.6e-2 / 0.964 to 1.8e-2 / 0.996, r5).
+    floor=(flat, cos): config 2's own shape (B = 32, C = 10), where the bf16 image tower's
+    rounding alone moves the gradients 6.0e-2 / cos 0.980 from fp32 (the backward-faithful
+    rounding oracle, round_bf16_fwd_bwd + round_f16_fwd_bwd) and where two evaluations of that
+    same rounded algorithm that differ only in accumulation precision (fp32 vs fp64) are already
+    5.0e-2 / 0.9848 apart (tools/summation_floor.py, profiles/r05/summation_floor.txt): the
+    adapter down-projection gradients sum ~6k rows through relu kinks and cancel. The GPU is
+    held to that floor against the rounding oracle (measured 4.8e-2 / 0.9845) — DESIGN.md §2."""
     from lcclip import OnlineTrainer
     cfg = o.VIT_B16
     sd = o.synthetic_state_dict(cfg, method, "both", seed=seed)
@@ -272,9 +274,19 @@ def _step_vs_oracle(dev, method, B, C, seed, tag):
     record(test=tag, method=method, B=B, C=C, **m)
     assert m["probs_abs_vs_fp32"] < 1e-2 and m["loss_abs"] < 1e-2, m
     check_logits(m)
-    assert flat < max(GRAD_REL, 1.25 * flat_o + 1e-2), m
-    for n in g32:
-        assert cos[n] >= min(0.99, cos_o[n] - 0.03), (n, cos[n], cos_o[n], e32[n], eo[n])
+    if floor is None:
+        # the north-star bound against the fp32 algorithm, no oracle-relative escape
+        assert flat < GRAD_REL, m
+        for n in g32:
+            assert cos[n] >= 0.99, (n, cos[n], e32[n])
+    else:
+        # bf16-image-tower-inherent (floor = the backward-faithful rounding oracle evaluated with
+        # fp32 vs fp64 accumulation, tools/summation_floor.py): the implementation is held to
+        # that floor against the rounding oracle, and to a sanity band against fp32
+        f_flat, f_cos = floor
+        assert flat_fb < 1.25 * f_flat, m
+        assert cos_fb[worst_fb] >= f_cos - 0.01, m
+        assert flat < 0.1 and min(cos.values()) >= 0.97, m
     return m
 
 
@@ -287,7 +299,7 @@ def test_lora_config1_shape_step_vs_oracle(dev):
 def test_adapter_config2_b32_step_vs_oracle(dev):
     """BASELINE config 2's method and prompt count (adapter both towers, C = 10) at B = 32: a
     larger batch than the B = 2 forward cases, the full train step against the oracle."""
-    _step_vs_oracle(dev, "adapter", 32, 10, 81, "adapter_b32_c10_step")
+    _step_vs_oracle(dev, "adapter", 32, 10, 81, "adapter_b32_c10_step", floor=(5.0e-2, 0.9848))
 
 
 def test_adapter_c100_step_vs_oracle(dev):
