@@ -204,10 +204,10 @@ class MaPLe(nn.Module):
             tokenized_prompts = self.tokenized_prompts
             prefix = self.token_prefix
             suffix = self.token_suffix
-        prompts, shared_ctx, deep_text, deep_vision = self.prompt_learner(prefix, suffix)
         vis = self.image_encoder
         side = self._text_stream(image)
         if side is None:
+            prompts, shared_ctx, deep_text, deep_vision = self.prompt_learner(prefix, suffix)
             text_features = self.text_encoder(prompts, tokenized_prompts, deep_text)
             image_features = lc_autograd.maple_image_apply(vis.tower, image, shared_ctx,
                                                            deep_vision, self.training)
@@ -217,18 +217,28 @@ class MaPLe(nn.Module):
             # the image tower, forward and backward (autograd runs each backward on its forward's
             # stream). The text function is applied after the image one so that its backward
             # (the higher sequence number) is launched first and overlaps the image backward.
+            # The prompt learner runs on the side stream too: its leaves (ctx, the deep text
+            # prompts, the projections) are then read on ONE stream, so their AccumulateGrad
+            # nodes and every gradient reaching them live on that stream (r4 read the deep text
+            # prompts on both streams: torch warned about the stream mismatch and inserted a
+            # cross-stream sync at every accumulation). The image tower waits for the learner's
+            # few small launches only.
             main = torch.cuda.current_stream(image.device)
-            ready = torch.cuda.Event()
-            ready.record(main)  # the prompt learner's outputs
+            if self.learner_on_side:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    prompts, shared_ctx, deep_text, deep_vision = self.prompt_learner(prefix, suffix)
+                learned = torch.cuda.Event()
+                learned.record(side)
+                main.wait_event(learned)
+                for t in (shared_ctx, *deep_vision):
+                    t.record_stream(main)
+            else:  # r4: the learner on the main stream (A/Bs)
+                prompts, shared_ctx, deep_text, deep_vision = self.prompt_learner(prefix, suffix)
+                side.wait_stream(main)
+                prompts.record_stream(side)
             image_features = lc_autograd.maple_image_apply(vis.tower, image, shared_ctx,
                                                            deep_vision, self.training)
-            side.wait_event(ready)
-            prompts.record_stream(side)
-            # (the deep text prompts are leaves read on both streams; their gradient from the text
-            # stream accumulates with torch's cross-stream sync, which warns once about the
-            # stream mismatch. Handing the text stream views made on this stream instead made
-            # autograd queue the text backward's join in front of the image backward: MaPLe
-            # 10.39 -> 11.45 ms per step, profiles/r04/t_*.log)
             with torch.cuda.stream(side):
                 text_features = self.text_encoder(prompts, tokenized_prompts, deep_text,
                                                   consumer=main)
@@ -239,6 +249,9 @@ class MaPLe(nn.Module):
 
     # the text tower on its own HIP stream beside the image tower (False: one stream, for A/Bs)
     overlap_text = True
+    # with overlap_text: the prompt learner on the text stream too (False: r4's main-stream
+    # learner, whose deep text prompts were read on both streams; for A/Bs)
+    learner_on_side = True
 
     def _text_stream(self, image):
         if not (self.overlap_text and image.is_cuda):

@@ -32,6 +32,7 @@ def run(prec):
     torch.manual_seed(0)
     m = MaPLe("ViT-B/16", n_ctx=3, device=dev, precision=prec)
     m.overlap_text = os.environ.get("OVERLAP", "1") != "0"  # text tower on its own stream
+    m.learner_on_side = os.environ.get("LEARNER_SIDE", "1") != "0"  # prompt learner there too
     m.train()
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand(B, 3, 224, 224, device=dev, generator=g)
