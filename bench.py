@@ -19,12 +19,22 @@ import os
 import sys
 import time
 
-# HIP hardware queues per process: 8 unless set (lcclip's own default, set here too because HIP
-# reads it when the runtime initialises, before lcclip is imported below): main, text-tower,
-# weight-gradient and RCCL streams each on their own queue. Recorded in the output line. With
-# fewer than 6 queues the trainer shares one side stream between the text tower and the PEFT
-# weight gradients (OnlineTrainer._merge_side_streams), which costs 6-12 % (profiles/r05/b/).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# HIP hardware queues per process: at least 8 (lcclip's own rule, applied here too because HIP
+# reads it when the runtime initialises, before lcclip is imported below; the GPU box exports
+# HIP's default, 4): main, text-tower, weight-gradient and RCCL streams each on their own queue.
+# Recorded in the output line. With fewer than 6 queues the trainer shares one side stream
+# between the text tower and the PEFT weight gradients (OnlineTrainer._merge_side_streams), which
+# costs 6-12 % (profiles/r05/b/).
+def _raise_hw_queues(n=8):
+    try:
+        cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        cur = 0
+    if cur < n:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(n)
+
+
+_raise_hw_queues()
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "lifelong-clip_amd")):
