@@ -34,7 +34,8 @@ def _raise_hw_queues(n=8):
         os.environ["GPU_MAX_HW_QUEUES"] = str(n)
 
 
-_raise_hw_queues()
+_raise_hw_queues(int(os.environ.get("LCCLIP_HW_QUEUES", "8")))  # (A/B knob: the minimum)
+HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")  # what HIP reads when it initialises below
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for p in (ROOT, os.path.join(ROOT, "lifelong-clip_amd")):
@@ -480,7 +481,7 @@ def main():
                          "note": "launches of the dominant kernel on the main (image-chain) "
                                  "stream, timed with HIP events around each launch of one extra "
                                  "eager step"},
-            "runtime": {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
+            "runtime": {"GPU_MAX_HW_QUEUES": HW_QUEUES,
                         "side_streams": 1 if trainer._merge_side_streams() else 2},
             "train_transform": tf_stats,
         }
