@@ -348,6 +348,9 @@ def main():
                     help="the text tower's 16-bit storage (AdapterCLIP text_precision)")
     ap.add_argument("--gemm-tile", type=int, default=0,
                     help="A/B knob: lc_gemm_set_tile value for every GEMM (0 = automatic)")
+    ap.add_argument("--streamk", type=int, default=None,
+                    help="A/B knob: lc_gemm_set_streamk mode (0 off, 1 N=768 K>=2048, 2 N=768, "
+                         "3 every ragged 256x256 launch; default: the library's)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -372,6 +375,10 @@ def main():
         from lcclip import _lib
         if _lib.load().lc_gemm_set_tile(args.gemm_tile) != 0:
             raise SystemExit(f"--gemm-tile {args.gemm_tile} rejected")
+    if args.streamk is not None:
+        from lcclip import _lib
+        if _lib.load().lc_gemm_set_streamk(args.streamk) != 0:
+            raise SystemExit(f"--streamk {args.streamk} rejected")
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
     model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev,

@@ -102,6 +102,14 @@ int lc_quant_fp8(hipStream_t stream, long rows, int K, const void* src, int src_
  * production library reads no environment variables.) */
 int lc_gemm_set_tile(int tile);
 
+/* Stream-K schedule of the 256x256 bf16 GEMM (plain / f32 / residual epilogues) for launches
+ * whose last round of tiles is ragged: one workgroup per CU, each owning an equal range of the
+ * launch's (tile, k-tile) units, a tile cut between two ranges summed through the split-K
+ * workspace. mode 0 = off, 1 = N = 768 with K >= 2048, 2 = every N = 768 launch, 3 = every
+ * ragged launch, 4 = N = 768 as one workgroup per 256-row panel walking its 3 column tiles.
+ * Process-wide; needs the launch's workspace (lc_gemm_nt_ws). */
+int lc_gemm_set_streamk(int mode);
+
 /* Diagnostic (builds with -DLC_GEMM_TRACE only): when p != NULL, the ping-pong GEMM stores
  * s_memtime stamps of its segments
  * (workgroup 0, waves 0 and 4) to p[512] (tools/gemm_trace.py). NULL disables (default). */

@@ -103,8 +103,11 @@ template <int BM, int BN, int WM, int WN, int EPI, int PASS_MAX = 32, int TM, in
 LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0, int n0, int M,
                        const float* __restrict__ bias, float alpha, void* __restrict__ out0,
                        long ldo0, void* __restrict__ out1, long ldo1, const void* __restrict__ aux,
-                       long ldaux, const EpiParams& ep) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                       long ldaux, const EpiParams& ep, int tid = -1) {
+  // tid: the caller's (opaque) thread id, so that a caller looping over tiles recomputes the
+  // lane-dependent addresses per tile instead of keeping them live (default: threadIdx.x)
+  if (tid < 0) tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   constexpr int NW = WM * WN;
 #if defined(G8_NOSTORE) && G8_NOSTORE == 1  // diagnostic builds only: epilogue off (results wrong)
@@ -765,7 +768,17 @@ gemm_pp_kernel(int M, int N, int K, const bf16_t* __restrict__ A, long lda,
 // lane passes the scale of block g). Conflict-free under the row XOR swizzle chunk ^ ((row >> 1) & 7).
 constexpr int TRACE_STAMPS_LOOP_END = 638;
 
-template <int EPI, bool FP8>
+// SKM (stream-K): gridDim.x workgroups, workgroup range r = an XCD-major renumbering of
+// blockIdx.x, owns the k-units [U r / G, U (r + 1) / G) of the T x KT units (tile-major), i.e.
+// whole tiles plus at most one partial tile at each end (the host guarantees U / G >= KT, so a
+// tile is cut at most once). The two parts of a cut tile meet through one slab per range
+// boundary b (between ranges b and b + 1) and a ticket: the first arriver writes its partial
+// (sc1 stores), drains, then adds 2 to the ticket; the second waits for the ticket to reach 4
+// (1 + 1 + 2), adds the slab (sc1 loads) to its registers, resets the ticket and runs the
+// epilogue. The wait is only ever on a workgroup that has already taken its ticket, i.e. is
+// resident and past its main loop. a + b = b + a in IEEE, so the result does not depend on
+// which part arrives first.
+template <int EPI, bool FP8, bool SKM = false>
 __global__ void __launch_bounds__(512, 1)
 gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
              const void* __restrict__ Bv, long ldb, const float* __restrict__ bias, float alpha,
@@ -787,26 +800,18 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 #endif
 
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;
   const int tiles_n = N / BN;
-  int bid = blockIdx.x;
-  int split = -1;
-  int tb = 0, te = K / KT;  // k-tiles [tb, te) of this workgroup
-  if (bid < sk.dp_tiles) {
-    const int nwg = sk.dp_tiles;
-    int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
-  } else {
-    int tail;
-    splitk_slice(bid - sk.dp_tiles, ((M + BM - 1) / BM) * tiles_n - sk.dp_tiles, sk.splits, tail,
-                 split);
-    bid = sk.dp_tiles + tail;
-    const int nt_all = K / KT;
-    tb = split * nt_all / sk.splits;
-    te = (split + 1) * nt_all / sk.splits;
-  }
+  // One tile (or k-slice of a tile): k-tiles [tb, te) of tile bid; split >= 0: slice `split` of
+  // a split-K tail tile; skb >= 0 (SKM): a cut tile meeting its other part at range boundary skb.
+  // Lane-dependent values are derived from an opaque copy of the thread id inside, so that hipcc
+  // cannot hoist them out of the SKM segment loop (they would stay live through the epilogue).
+  auto body = [&](int bid, int split, int tb, int te, int skb) {
+  int tid_o = tid;
+  if constexpr (SKM) asm volatile("" : "+v"(tid_o));
+  const int lane = tid_o & 63;
   int tm, tn;
   tile_coords(bid, (M + BM - 1) / BM, tiles_n, ep.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -1101,11 +1106,60 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
     }
     splitk_sum<TM, TN, 4>(acc, sk, tail, split, lane_off);
     stamp(632);
+  } else if (SKM && skb >= 0) {
+    // a cut tile (see the kernel comment): first arriver publishes, second adds and stores
+    constexpr int SLAB = BM * BN;
+    const int lane_off = (wave * TM * TN * 64 + lane) * 4;
+    int* tk = sk.tickets + skb;
+    int* flag = reinterpret_cast<int*>(smem);
+    __builtin_amdgcn_s_barrier();  // every wave done with the ring (lgkmcnt(0) above)
+    if (tid == 0) flag[0] = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int order = flag[0];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = lc_rsrc(sk.slabs + (long)skb * SLAB, (long)SLAB * 4);
+    if (order == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(lc_u32x4, acc[i][j]), rs,
+                                                 (lane_off + (i * TN + j) * 256) * 4, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(tk, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef LC_GEMM_CLOCK
+      clock_out();
+#endif
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(tk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 4)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < TM * TN; c += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane_off + (c + e) * 256) * 4, 0, 16));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[(c + e) / TN][(c + e) % TN] += v[e];
+      __builtin_amdgcn_sched_barrier(0);  // 4 slab loads in flight at a time (registers)
+    }
+    // its own epilogue call: merged with the whole-tile path, the summed accumulators came out
+    // of register allocation as copies with spills
+    store_tile<BM, BN, WM, WN, EPI>(acc, smem, 2 * BUF, m0, n0, M, bias, alpha, out0, ldo0, out1,
+                                    ldo1, aux, ldaux, ep, tid_o);
+    return;
   } else {
     __builtin_amdgcn_s_barrier();  // every wave done with the ring: the epilogue reuses it
   }
   store_tile<BM, BN, WM, WN, EPI>(acc, smem, 2 * BUF, m0, n0, M, bias, alpha, out0, ldo0, out1,
-                                  ldo1, aux, ldaux, ep);
+                                  ldo1, aux, ldaux, ep, SKM ? tid_o : -1);
 #ifdef LC_GEMM_TRACE
   stamp(TRACE_N - 1);
   __syncthreads();
@@ -1115,6 +1169,49 @@ gemm8_kernel(int M, int N, int K, const void* __restrict__ Av, long lda,
 #ifdef LC_GEMM_CLOCK
   clock_out();
 #endif
+  };  // body
+
+  const int nt_all = K / KT;
+  if constexpr (!SKM) {
+    int bid = blockIdx.x;
+    int split = -1;
+    int tb = 0, te = nt_all;  // k-tiles [tb, te) of this workgroup
+    if (bid < sk.dp_tiles) {
+      const int nwg = sk.dp_tiles;
+      int q = nwg / 8, r = nwg % 8, x = bid % 8, loc = bid / 8;
+      bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + loc;
+    } else {
+      int tail;
+      splitk_slice(bid - sk.dp_tiles, ((M + BM - 1) / BM) * tiles_n - sk.dp_tiles, sk.splits,
+                   tail, split);
+      bid = sk.dp_tiles + tail;
+      tb = split * nt_all / sk.splits;
+      te = (split + 1) * nt_all / sk.splits;
+    }
+    body(bid, split, tb, te, -1);
+  } else {
+    // XCD-major range numbering: ranges r and r + 1 (which may share a cut tile) run on the same
+    // XCD under round-robin placement, except where one XCD's block of ranges ends
+    const int G = gridDim.x, w = blockIdx.x;
+    const int r = (G % 8 == 0) ? (w % 8) * (G / 8) + w / 8 : w;
+    const long U = (long)((M + BM - 1) / BM) * tiles_n * nt_all;
+    long u = U * r / G;
+    const long ue = U * (r + 1) / G;
+    bool first = true;
+#pragma unroll 1
+    while (u < ue) {
+      const int tile = (int)(u / nt_all), k0 = (int)(u % nt_all);
+      const int k1 = (int)min((long)nt_all, k0 + (ue - u));
+      const int skb = (k0 == 0 && k1 == nt_all) ? -1 : (k0 == 0 ? r : r - 1);
+      if (!first) {  // the previous segment's epilogue staged through the ring
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      body(tile, -1, k0, k1, skb);
+      first = false;
+      u += k1 - k0;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1786,6 +1883,43 @@ SplitK plan_split(int tiles, int units, int min_units, void* ws, long ws_bytes, 
   return sk;
 }
 
+// Stream-K plan (gemm8_kernel<.., SKM>): one workgroup per CU, each owning U / G >= one tile of
+// k-units, cut tiles meeting through one slab per range boundary (G - 1 slabs and tickets in the
+// split-K workspace). Only for launches with a ragged last round of more than one tile per CU.
+// g_sk_mode (lc_gemm_set_streamk): 0 off, 1 N = 768 with K >= 2048, 2 every N = 768 launch,
+// 3 every ragged bf16 launch, 4 N = 768 as whole row panels (one workgroup per panel).
+int g_sk_mode = 0;
+bool plan_sk(int tiles, int units, void* ws, long ws_bytes, SplitK& sk, int& G, int panels = 0) {
+  G = panels > 0 ? panels : cu_count();
+  if (panels > 0 && tiles % panels == 0 && ws != nullptr) {  // whole row panels: no cut tiles
+    sk.dp_tiles = 0;
+    sk.splits = 1;
+    sk.tickets = static_cast<int*>(ws);
+    sk.slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
+    return true;
+  }
+  if (ws == nullptr || tiles <= G || tiles % G == 0) return false;
+  if ((long)tiles * units / G < units) return false;
+  if ((long)(G - 1) * 4 > LC_SPLITK_TICKET_BYTES ||
+      LC_SPLITK_TICKET_BYTES + (long)(G - 1) * 256 * 256 * 4 > ws_bytes)
+    return false;
+  sk.dp_tiles = 0;
+  sk.splits = 1;
+  sk.tickets = static_cast<int*>(ws);
+  sk.slabs = reinterpret_cast<float*>(static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES);
+  return true;
+}
+bool sk_wanted(int epi, int N, int K) {
+  if (epi != EPI_BF16 && epi != EPI_F32 && epi != EPI_RESID) return false;
+  switch (g_sk_mode) {
+    case 1: return N == 768 && K >= 2048;
+    case 2: return N == 768;
+    case 3: return true;
+    case 4: return N == 768;
+    default: return false;
+  }
+}
+
 // row panels per tile-raster group of the 256x256 GEMMs (tile_coords; env LC_GEMM_GM forces one).
 // Measured (tools/gpu_gm.sh, M = 50 432): groups of 8 panels help the wide-N shapes (QKV fwd
 // N = 2304: 181 -> 174 us, c_fc fwd N = 3072: 311 -> 303-307 us, c_proj dX -1 %) and cost the
@@ -1876,6 +2010,29 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
   const long ea = FP8 ? 1 : 2;  // bytes per element
   // the main-loop DMA descriptors span one 256-row tile of A / B with 32-bit byte offsets
   LC_CHECK_ARG(lda * ea < (1L << 23) && ldb * ea < (1L << 23));
+  if constexpr (!FP8) {
+    SplitK skm{};
+    int G = 0;
+    // mode 4: one workgroup per 256-row panel walking its N / 256 column tiles (hipBLASLt's
+    // N = 768 schedule: 197 workgroups at M = 50 432, no tile cut)
+    const int panels = g_sk_mode == 4 ? (M + 255) / 256 : 0;
+    if (sk_wanted(epi, N, K) && plan_sk(tiles, units, ws, ws_bytes, skm, G, panels)) {
+#define LC_G8SK_CASE(E)                                                                          \
+  case E:                                                                                        \
+    hipLaunchKernelGGL((gemm8_kernel<E, false, true>), dim3(G), dim3(512), 0, st, M, N, K, A,    \
+                       lda * ea, B, ldb * ea, bias, alpha, o0, l0, o1, l1, aux, la, ep, skm, sc); \
+    break;
+      switch (epi) {
+        LC_G8SK_CASE(EPI_BF16)
+        LC_G8SK_CASE(EPI_F32)
+        LC_G8SK_CASE(EPI_RESID)
+        default:
+          return LC_EINVAL;
+      }
+#undef LC_G8SK_CASE
+      LC_LAUNCH_RET();
+    }
+  }
   dim3 grid(sk.dp_tiles + (tiles - sk.dp_tiles) * sk.splits), block(512);
 #define LC_G8_CASE(E)                                                                          \
   case E:                                                                                      \
@@ -2070,6 +2227,12 @@ int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void*
 int lc_gemm_set_tile(int tile) {
   LC_CHECK_ARG(tile >= 0 && tile <= 11);
   g_force_tile = tile;
+  return LC_OK;
+}
+
+int lc_gemm_set_streamk(int mode) {
+  LC_CHECK_ARG(mode >= 0 && mode <= 4);
+  g_sk_mode = mode;
   return LC_OK;
 }
 

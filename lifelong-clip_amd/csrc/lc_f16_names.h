@@ -12,6 +12,7 @@
 #define lc_gemm_set_debug lc_gemm_set_debug_f16
 #define lc_gemm_nt_fp8 lc_gemm_nt_fp8_f16
 #define lc_gemm_set_tile lc_gemm_set_tile_f16
+#define lc_gemm_set_streamk lc_gemm_set_streamk_f16
 #define lc_gemm_tn lc_gemm_tn_f16
 #define lc_gemm_tn_ws lc_gemm_tn_ws_f16
 #define lc_adapter_wgrad lc_adapter_wgrad_f16

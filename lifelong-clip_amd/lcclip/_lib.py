@@ -26,6 +26,7 @@ SIGNATURES = {
                        P, c_float, P, c_long, P, c_long, P, c_long, P, c_long, P, c_long],
     "lc_quant_fp8": [P, c_long, c_int, P, c_int, c_long, c_long, P, c_long, P, c_long],
     "lc_gemm_set_tile": [c_int],
+    "lc_gemm_set_streamk": [c_int],
     "lc_gemm_set_debug": [P],
     "lc_adapter_bwd_set_form": [c_int],
     "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float],

@@ -123,6 +123,31 @@ def test_gemm_splitk_tail(ops, dev, M, N, K, tile):
         lib.lc_gemm_set_tile(0)
 
 
+@pytest.mark.parametrize("M,N,K", [(50432, 768, 3072), (50432, 768, 2304), (50432 - 37, 768, 768),
+                                   (25216, 768, 768), (296 * 256 - 100, 256, 2048)])
+@pytest.mark.parametrize("mode", [2, 3, 4])
+def test_gemm_streamk(ops, dev, M, N, K, mode):
+    """Stream-K schedule of the 256x256 kernel (lc_gemm_set_streamk): equal (tile, k-tile) ranges
+    per CU, tiles cut between two ranges summed through the workspace. Bit-exact on small
+    integers (plain and residual epilogues), tickets left zero, deterministic on random data;
+    mode 2 covers the N = 768 launches only (the N = 256 case then takes the split-K tail)."""
+    from lcclip import _lib
+    lib = _lib.load()
+    assert lib.lc_gemm_set_streamk(mode) == 0
+    assert lib.lc_gemm_set_streamk(5) != 0
+    try:
+        _splitk_tail(ops, dev, M, N, K)
+        g = torch.Generator(device=dev).manual_seed(11)
+        A = torch.randint(-3, 4, (M, K), device=dev, generator=g).to(BF)
+        B = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(BF)
+        res = torch.randint(-5, 6, (M, N), device=dev, generator=g).float()
+        out = torch.full((M, N), float("nan"), device=dev)
+        ops.gemm_nt(A, B, ops.EPI_RESID, out, aux=res)
+        assert torch.equal(out, A.float() @ B.float().t() + res)
+    finally:
+        lib.lc_gemm_set_streamk(0)
+
+
 def _splitk_tail(ops, dev, M, N, K):
     """The split-K tail of the 256x256 ping-pong GEMM (lc_gemm_nt_ws): these shapes leave the
     last round over 256 CUs at most half full (591 / 2364 / 296 tiles), so their tail tiles are

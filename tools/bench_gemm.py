@@ -1,8 +1,9 @@
 """GEMM microbenchmark on the ViT-B/16 step's shapes (dev tool): lc_gemm_nt tile variants,
 random bf16 operands, HIP-event timing on the launch stream, interleaved rounds.
 
-  VARIANTS=1,5,5n,8,f8  (5n = ping-pong without the split-K workspace, 8 = phase-interleaved
-  bf16 kernel, f8 = its block-scaled fp8 form on pre-quantised operands)   SQUARE=1 adds 4096^3/8192^3
+  VARIANTS=1,5,5n,8,f8,s3  (5n = ping-pong without the split-K workspace, 8 = phase-interleaved
+  bf16 kernel, f8 = its block-scaled fp8 form on pre-quantised operands, sK = the 8 kernel under
+  lc_gemm_set_streamk(K), hb = hipBLASLt through torch.matmul)   SQUARE=1 adds 4096^3/8192^3
 """
 import os
 import sys
@@ -66,7 +67,9 @@ reps = int(os.environ.get("REPS", 10))
 for rnd in range(3):
     for name, m, N, K, epi in SHAPES:
         for v in VARIANTS:
-            t = 8 if v in ("f8", "hb") else int(v.rstrip("n"))
+            t = 8 if v in ("f8", "hb") or v.startswith("s") else int(v.rstrip("n"))
+            if v.startswith("s") or hasattr(lib, "lc_gemm_set_streamk"):
+                lib.lc_gemm_set_streamk(int(v[1:]) if v.startswith("s") else 0)
             if t in (3, 5, 6, 7, 8) and N % 256:
                 continue
             if v != "hb" and lib.lc_gemm_set_tile(t) != 0:
@@ -90,6 +93,8 @@ for rnd in range(3):
             ms = e0.elapsed_time(e1) / reps
             res.setdefault((name, v), []).append(ms)
 lib.lc_gemm_set_tile(0)
+if hasattr(lib, "lc_gemm_set_streamk"):
+    lib.lc_gemm_set_streamk(0)
 for name, m, N, K, epi in SHAPES:
     line = f"{name:8s} M={m:6d} N={N:5d} K={K:5d}"
     for v in VARIANTS:
