@@ -351,6 +351,8 @@ def main():
     ap.add_argument("--streamk", type=int, default=None,
                     help="A/B knob: lc_gemm_set_streamk mode (0 off, 1 N=768 K>=2048, 2 N=768, "
                          "3 every ragged 256x256 launch; default: the library's)")
+    ap.add_argument("--resid32", action="store_true",
+                    help="A/B knob: the image tower's residual stream in f32 instead of IEEE half")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -379,6 +381,9 @@ def main():
         from lcclip import _lib
         if _lib.load().lc_gemm_set_streamk(args.streamk) != 0:
             raise SystemExit(f"--streamk {args.streamk} rejected")
+    if args.resid32:
+        from lcclip.engine import ImageTower
+        ImageTower.RESID16 = False
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
     model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev,
@@ -450,6 +455,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "text_tower_dtype": {"fp16": "f16", "bf16": "bf16"}[args.text_precision],
+            # the image tower's residual stream (the reference's autocast dtype: fp16)
+            "image_residual_dtype": "f16" if trainer.img._resid16() else "f32",
             "data": "synthetic (random-init ViT-B/16 CLIP weights, U[0,1) images normalised with "
                     "CIFAR-100 stats, random prompt token ids)",
             "config": {"workload": f"{args.method}_clip ViT-B/16 both towers, online_train step "

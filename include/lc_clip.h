@@ -170,6 +170,30 @@ int lc_layernorm_bwd_fp8(hipStream_t stream, int rows, int D, const void* dy, in
                          long ldo, const int* row_idx, void* q, long ldq, void* q_scale,
                          long q_rows);
 
+/* The image tower's residual stream in IEEE half (x16). The reference's residual stream is
+ * fp16 under autocast: its LayerNorm returns the input's dtype (model.py:194-200), conv1's
+ * output is fp16 (model.py:756-766) and every `x = x + ...` stays fp16 (model.py:439-442).
+ * The _x16 entry points take and return x as half [rows, ldx] (ldx % 4 == 0, 8-B aligned;
+ * 16-B for lc_adapter_ln_fwd_x16 with ldx % 8 == 0); the LayerNorm statistics are f32 and a
+ * LayerNorm of a stored x reads the rounded value. Everything else as the f32 forms. */
+int lc_layernorm_fwd_x16(hipStream_t stream, int rows, int D, const void* x, long ldx,
+                         const int* row_idx, const float* gamma, const float* beta, void* y,
+                         int y_f32, long ldy, float* mean, float* rstd);
+int lc_layernorm_bwd_x16(hipStream_t stream, int rows, int D, const void* dy, int dy_f32,
+                         long ldy, const void* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, float* dx, void* dx_bf16,
+                         long ldo, const int* row_idx);
+int lc_vit_embed_ln_x16(hipStream_t stream, int n_img, int n_patch, int D, const float* patch,
+                        const float* cls, const float* pos, const float* ln_pre_w,
+                        const float* ln_pre_b, void* x0, const float* ln1_w, const float* ln1_b,
+                        void* y, float* mean1, float* rstd1);
+int lc_adapter_ln_fwd_x16(hipStream_t stream, int M, int D, const void* z, long ldz,
+                          const void* Wd, const float* bd, const void* Wu, const float* bu,
+                          float scale, float keep, unsigned long long seed,
+                          const unsigned long long* seed_dev, const void* resid, void* xout,
+                          long ldx, void* hout, const float* gamma, const float* beta, void* y,
+                          long ldy, float* mean, float* rstd);
+
 /* im2col of NCHW f32 images into bf16 patches [n*g*g, 3*P*P] in conv1's (c, kh, kw) order.
  * Replaces: the input side of conv1 (model.py:756-758). */
 int lc_patchify(hipStream_t stream, int n_img, int res, int patch, const float* img, void* out);

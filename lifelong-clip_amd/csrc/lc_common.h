@@ -93,6 +93,23 @@ LC_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 #define LC_ONE16 ((short)0x3F80)  // 1.0
 #endif
 
+// The residual stream x of a tower: f32, or IEEE half (the reference's autocast dtype: its
+// LayerNorm returns the input dtype, model.py:194-200, so x stays fp16 from conv1 on,
+// model.py:756-766 and every `x = x + ...`). Independent of the 16-bit storage build above.
+// xres<T>: element type (float or _Float16); load / round / store through these helpers.
+typedef _Float16 lc_h16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 lc_h16x4 __attribute__((ext_vector_type(4)));
+LC_DEV float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+LC_DEV uint32_t pack2h(float lo, float hi) {  // round to nearest even
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((lc_f32x2){lo, hi}, lc_h16x2));
+}
+// the value a residual element of type XT holds (identity for f32)
+template <typename XT>
+LC_DEV float xround(float v) {
+  if constexpr (sizeof(XT) == 2) return (float)(_Float16)v;
+  else return v;
+}
+
 // Async 16-byte global -> LDS copy; LDS destination = wave-uniform base + lane * 16.
 LC_DEV void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(GLB_PTR(gsrc), LDS_PTR(lds_wave_base), 16, 0, 0);

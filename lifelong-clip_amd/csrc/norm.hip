@@ -66,6 +66,53 @@ LC_DEV void store_row_bf16(bf16_t* __restrict__ p, int lane, const float (&v)[V]
   }
 }
 
+// A residual-stream row (XT = float or _Float16, lc_common.h), same lane layouts as above.
+// nt: nontemporal loads (a saved activation read once)
+template <int V, typename XT>
+LC_DEV void load_row_x(const XT* __restrict__ p, int lane, float (&v)[V], bool nt = false) {
+  if constexpr (sizeof(XT) == 4) {
+    if constexpr (V % 4 == 0) {
+      if (nt) {
+#pragma unroll
+        for (int i = 0; i < V / 4; ++i) {
+          const f32x4 t = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>((const float*)p + i * 256 + lane * 4));
+          v[4 * i] = t[0]; v[4 * i + 1] = t[1]; v[4 * i + 2] = t[2]; v[4 * i + 3] = t[3];
+        }
+        return;
+      }
+    }
+    load_row_f32<V>((const float*)p, lane, v);
+  } else if constexpr (V % 4 == 0) {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i) {
+      const u32x2* q = reinterpret_cast<const u32x2*>((const uint16_t*)p + i * 256 + lane * 4);
+      const u32x2 t = nt ? __builtin_nontemporal_load(q) : *q;
+      v[4 * i] = h2f(t[0] & 0xffff); v[4 * i + 1] = h2f(t[0] >> 16);
+      v[4 * i + 2] = h2f(t[1] & 0xffff); v[4 * i + 3] = h2f(t[1] >> 16);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = h2f(((const uint16_t*)p)[i * 64 + lane]);
+  }
+}
+template <int V, typename XT>
+LC_DEV void store_row_x(XT* __restrict__ p, int lane, const float (&v)[V]) {
+  if constexpr (sizeof(XT) == 4) {
+    store_row_f32<V>((float*)p, lane, v);
+  } else if constexpr (V % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < V / 4; ++i)
+      *reinterpret_cast<uint2*>((uint16_t*)p + i * 256 + lane * 4) =
+          uint2{pack2h(v[4 * i], v[4 * i + 1]), pack2h(v[4 * i + 2], v[4 * i + 3])};
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i)
+      ((uint16_t*)p)[i * 64 + lane] = __builtin_bit_cast(uint16_t, (_Float16)v[i]);
+  }
+}
+
 // A row (V % 4 == 0 layout) as e4m3 codes + E8M0 scales in the fp8 GEMM operand format: a
 // 32-column block is 8 consecutive lanes' 4 values; the arithmetic is quant_fp8_kernel's
 // (quant.hip) on the bf16-rounded values, so the codes equal bf16 output + quant_fp8.
@@ -94,9 +141,9 @@ LC_DEV void store_row_fp8(uint8_t* __restrict__ p, uint8_t* __restrict__ scales,
 }
 
 // y (bf16 / f32, optional when q is set) and / or q: the fp8 operand of the next GEMM
-template <int V>
+template <int V, typename XT = float>
 __global__ void __launch_bounds__(256)
-ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __restrict__ row_idx,
+ln_fwd_kernel(int rows, const XT* __restrict__ x, long ldx, const int* __restrict__ row_idx,
               const float* __restrict__ gamma, const float* __restrict__ beta, void* __restrict__ y,
               int y_f32, long ldy, float* __restrict__ mean_out, float* __restrict__ rstd_out,
               uint8_t* __restrict__ qo, long ldq, uint8_t* __restrict__ q_scale, long q_rows) {
@@ -107,7 +154,7 @@ ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __rest
   const long src = row_idx ? (long)row_idx[row] : (long)row;
   // every load of the row issued before the first reduction: one HBM round trip per row
   float v[V], gm[V], bt[V];
-  load_row_f32<V>(x + src * ldx, lane, v);
+  load_row_x<V, XT>(x + src * ldx, lane, v);
   load_row_f32<V>(gamma, lane, gm);
   load_row_f32<V>(beta, lane, bt);
   float s = 0.f;
@@ -136,10 +183,10 @@ ln_fwd_kernel(int rows, const float* __restrict__ x, long ldx, const int* __rest
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; total = dres + dx.
-template <int V>
+template <int V, typename XT = float>
 __global__ void __launch_bounds__(256)
 ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
-              const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+              const XT* __restrict__ x, long ldx, const float* __restrict__ mean,
               const float* __restrict__ rstd, const float* __restrict__ gamma,
               const float* __restrict__ dres, float* __restrict__ dx, bf16_t* __restrict__ dxb,
               long ldo, const int* __restrict__ row_idx, uint8_t* __restrict__ qo, long ldq,
@@ -153,15 +200,7 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   if (dy_f32) load_row_f32<V>((const float*)dy + (long)row * ldy, lane, g);
   else load_row_bf16<V>((const bf16_t*)dy + (long)row * ldy, lane, g);
   // the forward's saved input, read once: nontemporal (step +0.5 %, profiles/r02/epilogue_knockout.txt)
-  if constexpr (V % 4 == 0) {
-#pragma unroll
-    for (int i = 0; i < V / 4; ++i) {
-      const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + xr * ldx + i * 256 + lane * 4));
-      xv[4 * i] = t[0]; xv[4 * i + 1] = t[1]; xv[4 * i + 2] = t[2]; xv[4 * i + 3] = t[3];
-    }
-  } else {
-    load_row_f32<V>(x + xr * ldx, lane, xv);
-  }
+  load_row_x<V, XT>(x + xr * ldx, lane, xv, true);
   load_row_f32<V>(gamma, lane, gm);
   // the residual gradient too, before the reductions (it was a second exposed round trip)
   float r[V];
@@ -237,12 +276,12 @@ __global__ void vit_assemble_kernel(int n_img, int np, int D, const float* __res
 // the residual stream) and ln_1(x0) (bf16, the QKV GEMM operand) with ln_1's statistics. The
 // separate path writes and re-reads the assembled rows and x0 (vit_assemble, ln_pre, ln_1:
 // ≈ 465 MB more HBM traffic at batch 256). Both LayerNorms two-pass, as ln_fwd_kernel.
-template <int V>
+template <int V, typename XT = float>
 __global__ void __launch_bounds__(256)
 vit_embed_ln_kernel(int rows, int np, const float* __restrict__ patch,
                     const float* __restrict__ cls, const float* __restrict__ pos,
                     const float* __restrict__ g_pre, const float* __restrict__ b_pre,
-                    float* __restrict__ x0, const float* __restrict__ g1,
+                    XT* __restrict__ x0, const float* __restrict__ g1,
                     const float* __restrict__ b1, bf16_t* __restrict__ y,
                     float* __restrict__ mean1, float* __restrict__ rstd1) {
   constexpr int D = V * 64;
@@ -274,8 +313,8 @@ vit_embed_ln_kernel(int rows, int np, const float* __restrict__ patch,
   for (int i = 0; i < V; ++i) v[i] += p[i];
   norm(v, m0, r0);
 #pragma unroll
-  for (int i = 0; i < V; ++i) v[i] = v[i] * r0 * ga[i] + be[i];
-  store_row_f32<V>(x0 + (long)row * D, lane, v);
+  for (int i = 0; i < V; ++i) v[i] = xround<XT>(v[i] * r0 * ga[i] + be[i]);  // ln_1 reads x0 as stored
+  store_row_x<V, XT>(x0 + (long)row * D, lane, v);
   load_row_f32<V>(g1, lane, ga);
   load_row_f32<V>(b1, lane, be);
   norm(v, m1, r1);
@@ -326,19 +365,26 @@ int grid_for(long work, int block) {
   return (int)(g < 1 ? 1 : g);
 }
 
-int ln_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy, const float* x,
+// x16: x (the forward's LayerNorm input, the residual stream) is IEEE half
+int ln_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy, const void* x,
            long ldx, const float* mean, const float* rstd, const float* gamma, const float* dres,
            float* dx, void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
-           void* q_scale, long q_rows) {
+           void* q_scale, long q_rows, int x16 = 0) {
   LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
   if (rows == 0) return LC_OK;
   dim3 grid((rows + 3) / 4), block(256);
   switch (D / 64) {
 #define LC_LN_B(V)                                                                              \
   case V:                                                                                      \
-    hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy, x, ldx,    \
-                       mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16, ldo, row_idx,            \
-                       (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);                            \
+    if (x16)                                                                                   \
+      hipLaunchKernelGGL((ln_bwd_kernel<V, _Float16>), grid, block, 0, st, rows, dy, dy_f32,   \
+                         ldy, (const _Float16*)x, ldx, mean, rstd, gamma, dres, dx,            \
+                         (bf16_t*)dx_bf16, ldo, row_idx, (uint8_t*)q, ldq, (uint8_t*)q_scale,   \
+                         q_rows);                                                               \
+    else                                                                                       \
+      hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy,          \
+                         (const float*)x, ldx, mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16,   \
+                         ldo, row_idx, (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);            \
     break;
     LC_LN_B(1) LC_LN_B(2) LC_LN_B(4) LC_LN_B(8) LC_LN_B(12) LC_LN_B(16)
     default:
@@ -351,17 +397,23 @@ int ln_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy
 
 extern "C" {
 
-static int ln_fwd(hipStream_t st, int rows, int D, const float* x, long ldx, const int* row_idx,
+static int ln_fwd(hipStream_t st, int rows, int D, const void* x, long ldx, const int* row_idx,
                   const float* gamma, const float* beta, void* y, int y_f32, long ldy, float* mean,
-                  float* rstd, void* q, long ldq, void* q_scale, long q_rows) {
+                  float* rstd, void* q, long ldq, void* q_scale, long q_rows, int x16 = 0) {
   LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
   if (rows == 0) return LC_OK;
   dim3 grid((rows + 3) / 4), block(256);
   switch (D / 64) {
 #define LC_LN_F(V)                                                                               \
   case V:                                                                                       \
-    hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, block, 0, st, rows, x, ldx, row_idx, gamma, beta, \
-                       y, y_f32, ldy, mean, rstd, (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);   \
+    if (x16)                                                                                    \
+      hipLaunchKernelGGL((ln_fwd_kernel<V, _Float16>), grid, block, 0, st, rows,                \
+                         (const _Float16*)x, ldx, row_idx, gamma, beta, y, y_f32, ldy, mean,     \
+                         rstd, (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);                     \
+    else                                                                                        \
+      hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, block, 0, st, rows, (const float*)x, ldx,      \
+                         row_idx, gamma, beta, y, y_f32, ldy, mean, rstd, (uint8_t*)q, ldq,      \
+                         (uint8_t*)q_scale, q_rows);                                             \
     break;
     LC_LN_F(1) LC_LN_F(2) LC_LN_F(4) LC_LN_F(8) LC_LN_F(12) LC_LN_F(16)
     default:
@@ -398,6 +450,25 @@ int lc_layernorm_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32
                 row_idx, nullptr, 0, nullptr, 0);
 }
 
+#ifndef LC_F16  // the image tower's half residual stream (bf16 storage build only)
+int lc_layernorm_fwd_x16(hipStream_t st, int rows, int D, const void* x, long ldx,
+                         const int* row_idx, const float* gamma, const float* beta, void* y,
+                         int y_f32, long ldy, float* mean, float* rstd) {
+  LC_CHECK_ARG(y != nullptr && x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0);
+  return ln_fwd(st, rows, D, x, ldx, row_idx, gamma, beta, y, y_f32, ldy, mean, rstd, nullptr, 0,
+                nullptr, 0, 1);
+}
+
+int lc_layernorm_bwd_x16(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
+                         const void* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, float* dx, void* dx_bf16,
+                         long ldo, const int* row_idx) {
+  LC_CHECK_ARG(x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0);
+  return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
+                row_idx, nullptr, 0, nullptr, 0, 1);
+}
+#endif
+
 int lc_layernorm_bwd_fp8(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
                          const float* x, long ldx, const float* mean, const float* rstd,
                          const float* gamma, const float* dres, float* dx, void* dx_bf16,
@@ -427,10 +498,10 @@ int lc_vit_assemble(hipStream_t st, int n_img, int n_patch, int D, const float* 
   LC_LAUNCH_RET();
 }
 
-int lc_vit_embed_ln(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
-                    const float* cls, const float* pos, const float* ln_pre_w,
-                    const float* ln_pre_b, float* x0, const float* ln1_w, const float* ln1_b,
-                    void* y, float* mean1, float* rstd1) {
+static int vit_embed_ln(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
+                        const float* cls, const float* pos, const float* ln_pre_w,
+                        const float* ln_pre_b, void* x0, const float* ln1_w, const float* ln1_b,
+                        void* y, float* mean1, float* rstd1, int x16) {
   LC_CHECK_ARG(n_img > 0 && n_patch > 0 && (D == 512 || D == 768 || D == 1024));
   LC_CHECK_ARG(patch && cls && pos && ln_pre_w && ln_pre_b && x0 && ln1_w && ln1_b && y && mean1 &&
                rstd1);
@@ -438,14 +509,38 @@ int lc_vit_embed_ln(hipStream_t st, int n_img, int n_patch, int D, const float* 
   LC_CHECK_ARG(rows < (1L << 31) - 4);
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
 #define LC_VE(V)                                                                                 \
-  hipLaunchKernelGGL(vit_embed_ln_kernel<V>, grid, block, 0, st, (int)rows, n_patch, patch, cls,  \
-                     pos, ln_pre_w, ln_pre_b, x0, ln1_w, ln1_b, (bf16_t*)y, mean1, rstd1)
+  if (x16)                                                                                       \
+    hipLaunchKernelGGL((vit_embed_ln_kernel<V, _Float16>), grid, block, 0, st, (int)rows,        \
+                       n_patch, patch, cls, pos, ln_pre_w, ln_pre_b, (_Float16*)x0, ln1_w, ln1_b,  \
+                       (bf16_t*)y, mean1, rstd1);                                                \
+  else                                                                                           \
+    hipLaunchKernelGGL(vit_embed_ln_kernel<V>, grid, block, 0, st, (int)rows, n_patch, patch,     \
+                       cls, pos, ln_pre_w, ln_pre_b, (float*)x0, ln1_w, ln1_b, (bf16_t*)y, mean1, \
+                       rstd1)
   if (D == 512) LC_VE(8);
   else if (D == 768) LC_VE(12);
   else LC_VE(16);
 #undef LC_VE
   LC_LAUNCH_RET();
 }
+
+int lc_vit_embed_ln(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
+                    const float* cls, const float* pos, const float* ln_pre_w,
+                    const float* ln_pre_b, float* x0, const float* ln1_w, const float* ln1_b,
+                    void* y, float* mean1, float* rstd1) {
+  return vit_embed_ln(st, n_img, n_patch, D, patch, cls, pos, ln_pre_w, ln_pre_b, x0, ln1_w, ln1_b,
+                      y, mean1, rstd1, 0);
+}
+
+#ifndef LC_F16
+int lc_vit_embed_ln_x16(hipStream_t st, int n_img, int n_patch, int D, const float* patch,
+                        const float* cls, const float* pos, const float* ln_pre_w,
+                        const float* ln_pre_b, void* x0, const float* ln1_w, const float* ln1_b,
+                        void* y, float* mean1, float* rstd1) {
+  return vit_embed_ln(st, n_img, n_patch, D, patch, cls, pos, ln_pre_w, ln_pre_b, x0, ln1_w, ln1_b,
+                      y, mean1, rstd1, 1);
+}
+#endif
 
 int lc_text_embed(hipStream_t st, int C, int L, int D, const int64_t* tokens, const float* emb,
                   const float* pos, float* x) {

@@ -889,12 +889,12 @@ lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats
 // is COUNTED: the stores issued after the last DMA stay in flight while the next block computes.
 // Down projection: wave w computes the 16 bottleneck columns 16 (w & 3) over the K half (w >> 2),
 // so the cross-wave sum is one partial per output (4 KiB of LDS instead of eight).
-template <int D>
+template <int D, int XB = 4>  // XB: bytes per residual element (4 f32, 2 IEEE half)
 struct AdLnLay {
   static constexpr int ZROW = D * 2;                 // z image row bytes
   static constexpr int ZIMG = 16 * ZROW;             // one 16-row z block
   static constexpr int ZP = ZIMG / 1024 / 8;         // z DMA pieces per wave
-  static constexpr int XIMG = 16 * D * 4;            // one 16-row resid block (f32, plain rows)
+  static constexpr int XIMG = 16 * D * XB;           // one 16-row resid block (plain rows)
   static constexpr int XP = XIMG / 1024 / 8;         // resid DMA pieces per wave
   static constexpr int Z_OFF = 0;                    // one z buffer
   static constexpr int X_OFF = ZIMG;                 // two resid buffers
@@ -917,17 +917,20 @@ LC_DEV void vmcnt_le() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int D>
+// XT: the residual stream's element type (float, or _Float16 — the reference's autocast
+// residual, lc_common.h): resid in, x_out out; the LayerNorm reads x_out as stored.
+template <int D, typename XT = float>
 __global__ void __launch_bounds__(512, 1)
 adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_t* __restrict__ Wd,
                       const float* __restrict__ bd, const bf16_t* __restrict__ Wu,
                       const float* __restrict__ bu, float scale, float keep, uint64_t seed,
                       const unsigned long long* __restrict__ seed_dev,
-                      const float* __restrict__ resid, float* __restrict__ xout, long ldx,
+                      const XT* __restrict__ resid, XT* __restrict__ xout, long ldx,
                       bf16_t* __restrict__ hout, const float* __restrict__ gamma,
                       const float* __restrict__ beta, bf16_t* __restrict__ y, long ldy,
                       float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-  using L = AdLnLay<D>;
+  constexpr int XB = (int)sizeof(XT);
+  using L = AdLnLay<D, XB>;
   constexpr int KS = L::KS, NU = L::NU;
   __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -981,17 +984,18 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
       glds16(z + (long)m * ldz + c * 8, dst + piece * 1024);
     }
   };
-  // resid block b -> resid buffer buf, plain row-major [16][D] f32 (the epilogue's 16-B reads of
-  // 16 rows at one column are spread by the row stride D*4 = 3 / 2 KiB: 2-way at worst)
+  // resid block b -> resid buffer buf, plain row-major [16][D] (the epilogue's reads of 16 rows
+  // at one column are spread by the row stride: 2-way at worst); 16-B chunks of EPC elements
+  constexpr int EPC = 16 / XB;
   auto dma_x = [&](int b, int buf) {
     char* dst = smem + L::X_OFF + buf * L::XIMG;
 #pragma unroll
     for (int pp = 0; pp < L::XP; ++pp) {
       const int piece = wave * L::XP + pp;
       const int idx = piece * 64 + lane;
-      const int row = idx / (D / 4), c4 = idx % (D / 4);
+      const int row = idx / (D / EPC), c = idx % (D / EPC);
       const int m = min(b * 16 + row, M - 1);
-      glds16(resid + (long)m * ldx + c4 * 4, dst + piece * 1024);
+      glds16(resid + (long)m * ldx + c * EPC, dst + piece * 1024);
     }
   };
   const uint32_t lds0 = lds_addr(smem);
@@ -1001,10 +1005,11 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
   };
   // stores issued after the last DMA of a full block, per wave: h (waves 0-1), mean and rstd
   // (wave 0), then NST full-row pieces (x_out 2 rows x D x 4 B and y 2 rows x D x 2 B, 1 KiB each)
+  constexpr int XPR = D * XB / 512;  // x_out pieces per wave (2 rows x D x XB bytes, 1-KiB each)
 #ifdef ADLN_KO  // (the knocked-out stores are not in flight: the counted waits below stay exact)
-  constexpr int NST = ((ADLN_KO & 1) ? 0 : 2 * D / 256) + ((ADLN_KO & 2) ? 0 : D / 256);
+  constexpr int NST = ((ADLN_KO & 1) ? 0 : XPR) + ((ADLN_KO & 2) ? 0 : D / 256);
 #else
-  constexpr int NST = 2 * D / 256 + D / 256;
+  constexpr int NST = XPR + D / 256;
 #endif
   const int tail = NST + (wave < 2 ? 1 : 0) + (wave == 0 ? 2 : 0);
 
@@ -1088,13 +1093,24 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     float s1 = 0.f;
     // resid of this lane's outputs from the DMA'd image
     f32x4 xr4[NU];
+    uint2 xh4[NU];  // (XB == 2: the 4 halves)
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int col = wave * (D / 8) + 16 * u + 4 * g;
-      asm volatile("ds_read_b128 %0, %1"
-                   : "=v"(xr4[u]) : "v"(lds0 + L::X_OFF + buf * L::XIMG + (t * D + col) * 4));
+      if constexpr (XB == 4)
+        asm volatile("ds_read_b128 %0, %1"
+                     : "=v"(xr4[u]) : "v"(lds0 + L::X_OFF + buf * L::XIMG + (t * D + col) * 4));
+      else
+        asm volatile("ds_read_b64 %0, %1"
+                     : "=v"(xh4[u]) : "v"(lds0 + L::X_OFF + buf * L::XIMG + (t * D + col) * 2));
     }
     lds_wait0();
+    if constexpr (XB == 2) {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        xr4[u] = f32x4{h2f(xh4[u].x & 0xffff), h2f(xh4[u].x >> 16), h2f(xh4[u].y & 0xffff),
+                       h2f(xh4[u].y >> 16)};
+    }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       f32x4 acc = mfma16(wuf[u][0], ha0, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -1107,7 +1123,7 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const float v = acc[rr] + prm[col + rr];
-        xo[u][rr] = xr[rr] + zf[rr] + scale * v;
+        xo[u][rr] = xround<XT>(xr[rr] + zf[rr] + scale * v);  // the LayerNorm reads x_out as stored
         s1 += xo[u][rr];
       }
     }
@@ -1126,7 +1142,7 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     // (the 8 rows of a write group on distinct banks); y image: [16][YSTR] bf16 rows (padded).
     const uint32_t xs = lds0 + L::X_OFF + buf * L::XIMG;
     const uint32_t ys = lds0 + L::Y_OFF;
-    {
+    if constexpr (XB == 4) {
       // this lane's 16-B chunk of row t for tile u: c = wave D/32 + 4u + g (wave D/32 is a
       // multiple of 8), so its swizzled position is a per-lane base for even / odd u plus u x 64 B
       static_assert((D / 32) % 8 == 0, "wave column block must be whole 128-B groups");
@@ -1136,6 +1152,17 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
       for (int u = 0; u < NU; ++u)
         asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"((u & 1) ? x1 : x0), "v"(xo[u]),
                      "n"(u * 64) : "memory");
+    } else {
+      // half image [16][2 D B]: 16-B chunk c of row r at (c & ~7) | ((c ^ r) & 7); this lane's
+      // 8 B of tile u are half g & 1 of chunk c = wave D/64 + 2u + (g >> 1)
+      const uint32_t xb = xs + t * D * 2 + (g & 1) * 8;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int c = wave * (D / 64) + 2 * u + (g >> 1);
+        const uint32_t a = xb + ((c & ~7) | ((c ^ t) & 7)) * 16;
+        asm volatile("ds_write_b64 %0, %1" ::"v"(a),
+                     "v"(uint2{pack2h(xo[u][0], xo[u][1]), pack2h(xo[u][2], xo[u][3])}) : "memory");
+      }
     }
     float mean = 0.f;
 #pragma unroll
@@ -1175,20 +1202,26 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
     lds_barrier();  // both images complete (and every st read done)
     {
       const int rows_here = min(16, M - r0);
-      const __amdgpu_buffer_rsrc_t rx = lc_rsrc(xout + (long)r0 * ldx, (long)rows_here * ldx * 4);
+      const __amdgpu_buffer_rsrc_t rx = lc_rsrc(xout + (long)r0 * ldx, (long)rows_here * ldx * XB);
       const __amdgpu_buffer_rsrc_t ry = lc_rsrc(y + (long)r0 * ldy, (long)rows_here * ldy * 2);
-      // wave w: rows 2w, 2w + 1; x_out D / 256 pieces of 64 chunks per row, then y's 2 x 2 D
-      // bytes as D / 256 pieces of 1 KiB — one row (or y) at a time: few registers in flight
-      constexpr int XPR = D / 256;
+      // wave w: rows 2w, 2w + 1; f32 x_out: D / 256 pieces of 64 chunks per row (h = 0, 1); half
+      // x_out: its 2 x 2 D bytes as D / 256 pieces of 1 KiB (h = 1 only); then y's 2 x 2 D bytes
+      // as D / 256 pieces (h = 2) — one row (or y) at a time: few registers in flight
+      constexpr int YPR = D / 256;
 #pragma unroll
-      for (int h = 0; h < 3; ++h) {
-        uint4 v[XPR];
+      for (int h = (XB == 4 ? 0 : 1); h < 3; ++h) {
+        uint4 v[YPR];
 #pragma unroll
-        for (int j = 0; j < XPR; ++j) {
-          if (h < 2) {
+        for (int j = 0; j < YPR; ++j) {
+          if (h < 2 && XB == 4) {
             const int r = 2 * wave + h, c = j * 64 + lane;
             asm volatile("ds_read_b128 %0, %1"
                          : "=v"(v[j]) : "v"(xs + r * D * 4 + ((c & ~7) | ((c ^ r) & 7)) * 16));
+          } else if (h < 2) {
+            const int bb = j * 1024 + lane * 16, r = 2 * wave + bb / (2 * D), o = bb % (2 * D);
+            const int c = o >> 4;
+            asm volatile("ds_read_b128 %0, %1"
+                         : "=v"(v[j]) : "v"(xs + r * D * 2 + ((c & ~7) | ((c ^ r) & 7)) * 16));
           } else {
             const int bb = j * 1024 + lane * 16, r = 2 * wave + bb / (2 * D), o = bb % (2 * D);
             asm volatile("ds_read_b128 %0, %1" : "=v"(v[j]) : "v"(ys + r * L::YSTR + o));
@@ -1196,12 +1229,17 @@ adapter_ln_fwd_kernel(int M, const bf16_t* __restrict__ z, long ldz, const bf16_
         }
         lds_wait0();
 #pragma unroll
-        for (int j = 0; j < XPR; ++j) {
+        for (int j = 0; j < YPR; ++j) {
           const lc_u32x4 d = lc_u32x4{v[j].x, v[j].y, v[j].z, v[j].w};
           if (h < 2) {
 #if !(defined(ADLN_KO) && (ADLN_KO & 1))  // (diagnostic builds: x_out stores off)
-            const int r = 2 * wave + h, c = j * 64 + lane;
-            __builtin_amdgcn_raw_buffer_store_b128(d, rx, (int)(r * ldx * 4 + c * 16), 0, 0);
+            if constexpr (XB == 4) {
+              const int r = 2 * wave + h, c = j * 64 + lane;
+              __builtin_amdgcn_raw_buffer_store_b128(d, rx, (int)(r * ldx * 4 + c * 16), 0, 0);
+            } else {
+              const int bb = j * 1024 + lane * 16, r = 2 * wave + bb / (2 * D), o = bb % (2 * D);
+              __builtin_amdgcn_raw_buffer_store_b128(d, rx, (int)(r * ldx * 2 + o), 0, 0);
+            }
 #else
             asm volatile("" ::"v"(d));
 #endif
@@ -1344,16 +1382,19 @@ int lc_adapter_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const 
                        nullptr, 0, resid, ldx, ep);
 }
 
-int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
-                      const float* bd, const void* Wu, const float* bu, float scale, float keep,
-                      unsigned long long seed, const unsigned long long* seed_dev,
-                      const float* resid, float* xout, long ldx, void* hout,
-                      const float* gamma, const float* beta, void* y, long ldy, float* mean,
-                      float* rstd) {
-  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldz % 8 == 0 && ldx % 4 == 0 && ldy % 8 == 0);
+static int adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
+                          const float* bd, const void* Wu, const float* bu, float scale,
+                          float keep, unsigned long long seed,
+                          const unsigned long long* seed_dev, const void* resid, void* xout,
+                          long ldx, void* hout, const float* gamma, const float* beta, void* y,
+                          long ldy, float* mean, float* rstd, int x16) {
+  const int xb = x16 ? 2 : 4;
+  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldz % 8 == 0 && ldx % (16 / xb) == 0 &&
+               ldy % 8 == 0);
   // x_out / y leave as 16-B pieces through descriptors over a 16-row block (32-bit offsets)
   LC_CHECK_ARG(ldx < (1L << 24) && ldy < (1L << 24));
-  LC_CHECK_ARG(((uintptr_t)xout & 15) == 0 && ((uintptr_t)y & 15) == 0);
+  LC_CHECK_ARG(((uintptr_t)xout & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+               ((uintptr_t)resid & 15) == 0);
   LC_CHECK_ARG(ldz >= D && ldx >= D && ldy >= D && keep > 0.f && keep <= 1.f);
   LC_CHECK_ARG(z && Wd && bd && Wu && bu && resid && xout && hout && gamma && beta && y && mean && rstd);
   int dev = 0, cus = 256;
@@ -1362,16 +1403,43 @@ int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, con
     cus = 256;
   const int nblk = (M + 15) / 16;
   const int grid = nblk < cus ? nblk : cus;
-#define LC_ALN(DD)                                                                               \
-  hipLaunchKernelGGL(adapter_ln_fwd_kernel<DD>, dim3(grid), dim3(512), 0, st, M,                 \
+#define LC_ALN(DD, XT)                                                                           \
+  hipLaunchKernelGGL((adapter_ln_fwd_kernel<DD, XT>), dim3(grid), dim3(512), 0, st, M,           \
                      (const bf16_t*)z, ldz, (const bf16_t*)Wd, bd, (const bf16_t*)Wu, bu, scale,  \
-                     keep, (uint64_t)seed, seed_dev, resid, xout, ldx, (bf16_t*)hout, gamma,     \
-                     beta, (bf16_t*)y, ldy, mean, rstd)
-  if (D == 768) LC_ALN(768);
-  else LC_ALN(512);
+                     keep, (uint64_t)seed, seed_dev, (const XT*)resid, (XT*)xout, ldx,           \
+                     (bf16_t*)hout, gamma, beta, (bf16_t*)y, ldy, mean, rstd)
+  if (x16) {
+    if (D == 768) LC_ALN(768, _Float16);
+    else LC_ALN(512, _Float16);
+  } else {
+    if (D == 768) LC_ALN(768, float);
+    else LC_ALN(512, float);
+  }
 #undef LC_ALN
   LC_LAUNCH_RET();
 }
+
+int lc_adapter_ln_fwd(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
+                      const float* bd, const void* Wu, const float* bu, float scale, float keep,
+                      unsigned long long seed, const unsigned long long* seed_dev,
+                      const float* resid, float* xout, long ldx, void* hout,
+                      const float* gamma, const float* beta, void* y, long ldy, float* mean,
+                      float* rstd) {
+  return adapter_ln_fwd(st, M, D, z, ldz, Wd, bd, Wu, bu, scale, keep, seed, seed_dev, resid, xout,
+                        ldx, hout, gamma, beta, y, ldy, mean, rstd, 0);
+}
+
+#ifndef LC_F16  // the image tower's half residual stream (bf16 storage build only)
+int lc_adapter_ln_fwd_x16(hipStream_t st, int M, int D, const void* z, long ldz, const void* Wd,
+                          const float* bd, const void* Wu, const float* bu, float scale,
+                          float keep, unsigned long long seed,
+                          const unsigned long long* seed_dev, const void* resid, void* xout,
+                          long ldx, void* hout, const float* gamma, const float* beta, void* y,
+                          long ldy, float* mean, float* rstd) {
+  return adapter_ln_fwd(st, M, D, z, ldz, Wd, bd, Wu, bu, scale, keep, seed, seed_dev, resid, xout,
+                        ldx, hout, gamma, beta, y, ldy, mean, rstd, 1);
+}
+#endif
 
 static int g_adapter_bwd_fused = 1;
 

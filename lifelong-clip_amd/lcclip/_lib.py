@@ -87,6 +87,9 @@ F16_ENTRY_POINTS = ("lc_gemm_nt", "lc_gemm_nt_ws", "lc_gemm_tn", "lc_gemm_tn_ws"
                     "lc_adapter_ln_fwd", "lc_adapter_bwd", "lc_adapter_wgrad",
                     "lc_adapter_wgrad_ws")
 SIGNATURES.update({n + "_f16": SIGNATURES[n] for n in F16_ENTRY_POINTS})
+# the image tower's half residual stream (include/lc_clip.h "x16"): the f32 forms' arguments
+SIGNATURES.update({n + "_x16": SIGNATURES[n] for n in (
+    "lc_layernorm_fwd", "lc_layernorm_bwd", "lc_vit_embed_ln", "lc_adapter_ln_fwd")})
 
 _lib = None
 

@@ -247,8 +247,10 @@ class BlockStack:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False, prompts=None,
-                stop=None, replace=None, first_ln1=None):
-        """x: f32 [n_seq*L, D] residual stream. Returns (x_out, saved-per-layer or None).
+                stop=None, replace=None, first_ln1=None, last_ln=None):
+        """x: f32 [n_seq*L, D] residual stream, or float16 (the reference's autocast residual
+        dtype, model.py:194-200 / 439-442: the fused adapter tower only, with last_ln). Returns
+        (x_out, saved-per-layer or None).
 
         prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
         before that layer and dropped after it (prompt tuning, models/mvp_clip.py:158-175: cat
@@ -258,9 +260,12 @@ class BlockStack:
         overwritten before that layer (MaPLe's deep compound prompts,
         models/maple_clip/model.py:352-395). first_ln1: (y bf16 [M, D], mean, rstd) — the first
         block's ln_1 of x already computed (ops.vit_embed_ln), used when that block runs on x
-        unchanged (no prompt rows appended or replaced there, bf16 operands)."""
+        unchanged (no prompt rows appended or replaced there, bf16 operands). last_ln: {w, b, y,
+        mean, rstd} — the LayerNorm after the stack (ln_post) fused into the last block's
+        adapter (ops.adapter_ln_fwd): y bf16 [M, D] and its statistics over every row."""
         self.stage()
         M, D = x.shape
+        xdt = x.dtype  # the residual stream's
         H = self.n_head
         dev = x.device
         P_of = {int(i): int(t.shape[1]) for i, t in (prompts or {}).items()}
@@ -275,6 +280,10 @@ class BlockStack:
         # (ops.adapter_ln_fwd: ln_2 of the block, ln_1 of the next one); ln1_ready carries the
         # statistics of an ln_1 the previous block already wrote into tmp_h
         fuse_ln = (self.variant == "adapter" and q_h is None and D in (512, 768) and self.FUSE_LN)
+        if xdt != F32 and not (fuse_ln and q_g is None and last_ln is not None and not prompts
+                               and not replace and stop is None):
+            raise ValueError("a half residual stream runs the fused adapter tower only (no "
+                             "prompts, no fp8, the stack's closing LayerNorm fused: last_ln)")
         ln1_ready = None
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
             if stop is not None and idx >= stop:
@@ -316,7 +325,7 @@ class BlockStack:
             O = _empty((Mx, D), self.dt, dev)
             lse = _empty((n_seq * H, Lx), F32, dev)
             ops.attn_fwd(qkv, O, lse, n_seq, Lx, H, self.causal)
-            x_mid = _empty((Mx, D), F32, dev)
+            x_mid = _empty((Mx, D), xdt, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 keep = 1.0 - ad.dropout if (training and ad.dropout > 0) else 1.0
@@ -361,7 +370,7 @@ class BlockStack:
                 self._gemm(st, "wfc", th, EPI_GELU_D if save else EPI_GELU, pre,
                            bias=blk.mlp.c_fc.bias, out1=tmp_g[:Mx])
                 wpr = lambda epi, out0, **kw: self._gemm(st, "wpr", tmp_g[:Mx], epi, out0, **kw)  # noqa: E731
-            x_out = _empty((Mx, D), F32, dev)
+            x_out = _empty((Mx, D), xdt, dev)
             if self.variant == "adapter":
                 ad = blk.adaptmlp
                 seed2 = next(_seed_counter) * 0x9E3779B1
@@ -380,6 +389,14 @@ class BlockStack:
                                        nb.ln_1.weight, nb.ln_1.bias, th, m1, r1,
                                        seed_dev=self.seed_dev)
                     ln1_ready = (m1, r1)
+                elif (last_ln is not None and fuse_ln and nxt == len(self.blocks) and not P
+                      and stop is None):
+                    # the LayerNorm after the stack (ln_post) over every row
+                    ops.adapter_ln_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias,
+                                       ad.scale, s["keep"], seed2, x_mid, x_out, hd2,
+                                       last_ln["w"], last_ln["b"], last_ln["y"], last_ln["mean"],
+                                       last_ln["rstd"], seed_dev=self.seed_dev)
+                    last_ln["done"] = True
                 else:
                     ops.adapter_fwd(z2, st.wd, ad.down_proj.bias, st.wu, ad.up_proj.bias, ad.scale,
                                     s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
@@ -780,7 +797,7 @@ class ImageTower:
                              "storage is the text tower's")
         if (self.FUSE_EMBED and not prompts and self.stack.precision == "bf16"
                 and self.visual.width in (512, 768, 1024)):
-            x0, n, L, first = self.embed_ln1(img)
+            x0, n, L, first = self.embed_ln1(img, half=self._resid16())
             return self.forward_embedded(x0, n, L, save, training, prompts, first_ln1=first)
         x0, n, L = self.embed(img)
         return self.forward_embedded(x0, n, L, save, training, prompts)
@@ -788,15 +805,26 @@ class ImageTower:
     # the patch embedding's CLS / positional add, ln_pre and the first ln_1 in one launch
     # (False: the three separate launches, for A/Bs)
     FUSE_EMBED = True
+    # the residual stream in IEEE half, the reference's autocast dtype (model.py:194-200: its
+    # LayerNorm returns the input dtype, so x is fp16 from conv1 through every block; here the
+    # fused adapter tower: lc_*_x16): a third less HBM traffic in the fused adapter + LayerNorm
+    # forward and the x read of every LayerNorm backward. False: the f32 stream (A/Bs)
+    RESID16 = True
 
-    def embed_ln1(self, img):
+    def _resid16(self):
+        st = self.stack
+        return (self.RESID16 and self.FUSE_EMBED and st.variant == "adapter" and st.FUSE_LN
+                and st.precision == "bf16" and self.visual.width in (512, 768))
+
+    def embed_ln1(self, img, half=False):
         """embed() and the first block's ln_1 in one launch (ops.vit_embed_ln): (x0, n, L,
-        (ln_1(x0) bf16, mean1, rstd1)) for BlockStack.forward(first_ln1=...)."""
+        (ln_1(x0) bf16, mean1, rstd1)) for BlockStack.forward(first_ln1=...). half: x0 in IEEE
+        half (the half residual stream)."""
         v = self.visual
         pe, n, npch = self._patch_embed(img)
         L, D = npch + 1, v.width
         dev = pe.device
-        x0 = _empty((n * L, D), F32, dev)
+        x0 = _empty((n * L, D), F16 if half else F32, dev)
         y = _empty((n * L, D), BF16, dev)
         mean1 = _empty((n * L,), F32, dev)
         rstd1 = _empty((n * L,), F32, dev)
@@ -809,9 +837,20 @@ class ImageTower:
                          replace=None, first_ln1=None):
         """forward() from a precomputed embed() (the MVP query and prompt passes share x0)."""
         self._stage()
+        last = None
+        if x0.dtype == F16:  # ln_post fused into the last block's adapter over every row
+            v = self.visual
+            M, D = x0.shape
+            last = dict(w=v.ln_post.weight, b=v.ln_post.bias, y=_empty((M, D), BF16, x0.device),
+                        mean=_empty((M,), F32, x0.device), rstd=_empty((M,), F32, x0.device))
         x, saved = self.stack.forward(x0, n, L, save, training, prompts=prompts, replace=replace,
-                                      first_ln1=first_ln1)
-        lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
+                                      first_ln1=first_ln1, last_ln=last)
+        if last is not None and last.get("done"):
+            cls_idx = torch.arange(n, device=x.device, dtype=torch.int32) * L
+            ci = cls_idx.long()
+            lnp, mean, rstd = last["y"][ci], last["mean"][ci], last["rstd"][ci]
+        else:
+            lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
         f = _empty((n, self.projT.shape[0]), F32, x.device)
         ops.gemm_nt(lnp, self.projT, EPI_F32, f)
         ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L,

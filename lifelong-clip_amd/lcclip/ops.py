@@ -177,11 +177,27 @@ def gemm_tn(A, B, C, alpha=1.0, colsum=None, colsum_scale=1.0):
     return C
 
 
+def _x16(name, x, *ts):
+    """`name` for an f32 residual stream x, `name`_x16 for IEEE half x (the image tower's,
+    include/lc_clip.h; bf16 / f32 partners only)."""
+    if x.dtype == F32:
+        return _sym16(name, *ts)
+    if x.dtype != F16:
+        raise TypeError(f"{name}: residual stream x must be f32 or float16, got {x.dtype}")
+    if any(t is not None and t.dtype == F16 for t in ts):
+        raise TypeError(f"{name}: a half residual stream takes bf16 / f32 partners")
+    if x.stride(-1) != 1 or x.stride(0) % 4 or x.data_ptr() % 8:
+        raise ValueError(f"{name}: half x must be row-major, 8-B aligned, row stride % 4 == 0")
+    return name + "_x16"
+
+
 def layernorm_fwd(x, weight, bias, y, mean=None, rstd=None, row_idx=None):
-    _rowmajor(x, F32, "x")
+    """x: f32 or float16 (the image tower's half residual stream) [*, D]."""
+    if x.dtype != F16:
+        _rowmajor(x, F32, "x")
     rows = y.shape[0]
     D = x.shape[1]
-    call(_sym16("lc_layernorm_fwd", y), stream_of(x), rows, D, ptr(x), x.stride(0), ptr(row_idx),
+    call(_x16("lc_layernorm_fwd", x, y), stream_of(x), rows, D, ptr(x), x.stride(0), ptr(row_idx),
          ptr(weight), ptr(bias), ptr(y), 1 if y.dtype == F32 else 0, y.stride(0), ptr(mean),
          ptr(rstd))
     return y
@@ -201,9 +217,10 @@ def layernorm_fwd_fp8(x, weight, bias, q, mean=None, rstd=None, y=None):
 
 
 def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_idx=None):
+    """x: the forward's input, f32 or float16 (the half residual stream)."""
     rows = dy.shape[0]
     D = x.shape[1]
-    call(_sym16("lc_layernorm_bwd", dy, dx_bf16), stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+    call(_x16("lc_layernorm_bwd", x, dy, dx_bf16), stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
          dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
          ptr(dx_bf16), dx.stride(0), ptr(row_idx))
     return dx
@@ -240,11 +257,11 @@ def vit_assemble(patch_emb, cls, pos, x, n_img, n_patch):
 
 def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, mean1, rstd1,
                  n_img, n_patch):
-    """vit_assemble + ln_pre -> x0 (f32) and the first block's ln_1 -> y (bf16), mean1, rstd1,
-    in one launch (lc_vit_embed_ln)."""
+    """vit_assemble + ln_pre -> x0 (f32, or float16: the half residual stream) and the first
+    block's ln_1 -> y (bf16), mean1, rstd1, in one launch (lc_vit_embed_ln[_x16])."""
     D = x0.shape[1]
     rows = n_img * (n_patch + 1)
-    if tuple(x0.shape) != (rows, D) or tuple(y.shape) != (rows, D) or x0.dtype != F32 \
+    if tuple(x0.shape) != (rows, D) or tuple(y.shape) != (rows, D) or x0.dtype not in (F32, F16) \
             or y.dtype != BF16 or not x0.is_contiguous() or not y.is_contiguous() \
             or tuple(patch_emb.shape) != (n_img * n_patch, D) or not patch_emb.is_contiguous():
         raise ValueError("vit_embed_ln: shape / layout mismatch")
@@ -255,7 +272,7 @@ def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, m
         if t.dtype != F32 or not t.is_contiguous() or t.numel() != numel or t.device != x0.device:
             raise ValueError(f"vit_embed_ln: {name} must be contiguous f32 with {numel} elements "
                              f"on {x0.device}")
-    call("lc_vit_embed_ln", stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
+    call(_x16("lc_vit_embed_ln", x0), stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
          ptr(ln_pre_w), ptr(ln_pre_b), ptr(x0), ptr(ln1_w), ptr(ln1_b), ptr(y), ptr(mean1),
          ptr(rstd1))
     return x0
@@ -420,11 +437,17 @@ def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=N
 
 def adapter_ln_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, gamma, beta, y, mean,
                    rstd, seed_dev=None):
-    """adapter_fwd, then y = LayerNorm(xout) (bf16, statistics saved) in one launch."""
+    """adapter_fwd, then y = LayerNorm(xout) (bf16, statistics saved) in one launch. resid /
+    xout: f32, or float16 (the image tower's half residual stream; xout row stride % 8 == 0)."""
     M, D = z.shape
     if y.dtype != z.dtype or tuple(y.shape) != (M, D) or y.stride(1) != 1:
         raise ValueError("adapter_ln_fwd: y must be a [M, D] row-major view of z's 16-bit type")
-    call(_sym16("lc_adapter_ln_fwd", z, Wd, Wu, h, y), stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
+    if resid.dtype != xout.dtype or tuple(resid.shape) != (M, D) or tuple(xout.shape) != (M, D) \
+            or resid.stride() != xout.stride():
+        raise ValueError("adapter_ln_fwd: resid and xout must be [M, D] views of one dtype and stride")
+    if xout.dtype == F16 and (xout.stride(0) % 8 or xout.data_ptr() % 16 or resid.data_ptr() % 16):
+        raise ValueError("adapter_ln_fwd: half xout / resid rows must be 16-B aligned pieces")
+    call(_x16("lc_adapter_ln_fwd", xout, z, Wd, Wu, h, y), stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
          ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
          ptr(resid), ptr(xout), xout.stride(0), ptr(h), ptr(gamma), ptr(beta), ptr(y),
          y.stride(0), ptr(mean), ptr(rstd))

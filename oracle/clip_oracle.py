@@ -90,6 +90,14 @@ def round_f16(x):
     return x + (r - x).detach()
 
 
+# The MI355X image tower keeps the fused adapter tower's residual stream in IEEE half, the
+# reference's autocast dtype (model.py:194-200: its LayerNorm returns the input dtype, so x is
+# fp16 from conv1 through every `x = x + ...`; lcclip ImageTower.RESID16, widths 512 / 768):
+# encode_image rounds x there with the image rounding's ``resid`` hook (straight-through: the
+# residual gradient stays f32 on the GPU).
+round_bf16.resid = round_f16
+
+
 class _GradRound(torch.autograd.Function):
     """Identity forward; the incoming gradient rounded by `rnd`: a point where the HIP backward
     stores a 16-bit gradient that the next GEMM reads."""
@@ -193,6 +201,8 @@ class Rounding:
         self.kind = kind
         self._rnd = {"bf16": _bf, "f16": _hf}[kind]
         self.gs = 1.0
+        if kind == "bf16":
+            self.resid = round_f16  # the image tower's half residual stream (round_bf16.resid)
         if backward:
             self.bwd = lambda x: _GradRound.apply(x, self._grnd)
             self.gelu = lambda x: _QuickGeluRound.apply(x, self._rnd)
@@ -470,10 +480,11 @@ def adapter(z, p, pre, scale=0.1, dropout_mask=None, rt=identity):
     return z + scale * u
 
 
-def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, masks=None):
+def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, masks=None,
+          xr=identity):
     """ResidualAttentionBlock{,_LoRA} forward (model.py:233-236) and _Adapter forward
-    (model.py:439-442; one adapter module reused for both sub-blocks, Q6). x is the fp32
-    residual stream [N, L, D]."""
+    (model.py:439-442; one adapter module reused for both sub-blocks, Q6). x is the residual
+    stream [N, L, D]; xr rounds it after each residual add (the half residual stream)."""
     # gq: the backward's bf16 gradient stores (rt.bwd; identity for the fp32 oracle and the
     # straight-through round_bf16): the residual stream's gradient stays f32 and each sub-block
     # reads its bf16 copy (dx_midb / the layer's output pair, engine.py BlockStack.backward);
@@ -484,18 +495,18 @@ def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, ma
     a = mha(h, p, pre, n_head, causal, lora_scaling if variant == "lora" else None, rt)
     if variant == "adapter":
         m0 = None if masks is None else masks[0]
-        x = x + gq(adapter(gq(rt(a)), p, pre, dropout_mask=m0, rt=rt))
+        x = xr(x + gq(adapter(gq(rt(a)), p, pre, dropout_mask=m0, rt=rt)))
     else:
-        x = x + gq(a)
+        x = xr(x + gq(a))
     h2 = gq(rt(layer_norm(x, p[pre + "ln_2.weight"], p[pre + "ln_2.bias"])))
     f = rt(gelu(gq(linear(h2, p[pre + "mlp.c_fc.weight"], p[pre + "mlp.c_fc.bias"], rt,
                           fp8=True))))
     m = linear(f, p[pre + "mlp.c_proj.weight"], p[pre + "mlp.c_proj.bias"], rt, fp8=True)
     if variant == "adapter":
         m1 = None if masks is None else masks[1]
-        x = x + gq(adapter(gq(rt(m)), p, pre, dropout_mask=m1, rt=rt))
+        x = xr(x + gq(adapter(gq(rt(m)), p, pre, dropout_mask=m1, rt=rt)))
     else:
-        x = x + gq(m)
+        x = xr(x + gq(m))
     return x
 
 
@@ -517,12 +528,15 @@ def encode_image(img, p, cfg: ClipConfig, method="vanilla", peft_encoder="none",
     cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
     x = torch.cat([cls, x], dim=1)                                              # :759-763
     x = x + p["visual.positional_embedding"]                                    # :764
-    x = layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])      # :766
     variant = tower_variant(method, peft_encoder, "image")
+    # the MI355X fused adapter tower's half residual stream (round_bf16.resid above)
+    xr = (getattr(rt, "resid", identity)
+          if variant == "adapter" and cfg.vision_width in (512, 768) else identity)
+    x = xr(layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"]))  # :766
     vis, _ = tower_prefixes(cfg)
     for i, pre in enumerate(vis):
         x = block(x, p, pre, cfg.vision_heads, False, variant, rt=rt,
-                  masks=None if masks is None else masks[i])
+                  masks=None if masks is None else masks[i], xr=xr)
     tail = getattr(rt, "tail", rt)  # rounding of ln_post's output and the projection GEMM
     x = tail(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))  # :783
     # the feature gradient is cast to 16 bits before the projection's backward GEMM

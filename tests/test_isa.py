@@ -6,7 +6,8 @@ adapter_ln_fwd_kernel (peft.hip) waits at the top of each 16-row block with a CO
 LDS-DMAs must have landed. CDNA retires vector-memory ops in issue order, so the count is right
 only while the loop issues exactly `tail` stores after its last LDS-DMA — NST + 3 on the waves
 that store everything: the h block (16 B), mean and rstd (4 B each), then x_out and y as whole-row
-1-KiB pieces through buffer descriptors (NST = 2 D / 256 + D / 256 per wave; hipcc rotates the
+1-KiB pieces through buffer descriptors (NST = 2 D / 256 + D / 256 per wave, D / 256 + D / 256
+with the half residual stream; hipcc rotates the
 loop, so those appear above the loop header in the text). Fewer stores emitted (e.g. two merged)
 would let a read of a slot whose DMA has not landed through, silently; more would only make the
 wait conservative. This test pins the emitted count to the one the kernel source assumes
@@ -44,15 +45,18 @@ def function_body(asm, pattern):
 
 
 @pytest.mark.parametrize("D", [768, 512])
-def test_adapter_ln_fwd_store_tail_matches_wait(peft_asm, D):
-    body = function_body(peft_asm, rf"_ZN12_GLOBAL__N_121adapter_ln_fwd_kernelILi{D}E")
+@pytest.mark.parametrize("xt", ["f", "DF16_"])
+def test_adapter_ln_fwd_store_tail_matches_wait(peft_asm, D, xt):
+    """xt: the residual element type (f32, or IEEE half: x_out is then D / 256 pieces per wave
+    instead of 2 D / 256)."""
+    body = function_body(peft_asm, rf"_ZN12_GLOBAL__N_121adapter_ln_fwd_kernelILi{D}E{xt}E")
     lines = [ln.strip() for ln in body.splitlines()]
     dma = [i for i, ln in enumerate(lines) if ln.startswith("global_load_lds") or
            (ln.startswith("buffer_load") and " lds" in ln)]
     assert dma, "no LDS-DMA in the kernel"
     tail = [ln.split()[0] for ln in lines[dma[-1] + 1:]
             if ln.startswith(("global_store", "buffer_store"))]
-    NST = 2 * D // 256 + D // 256
+    NST = (2 * D // 256 if xt == "f" else D // 256) + D // 256
     # h block (16 B, waves 0-1), mean / rstd (wave 0) after the last DMA in the text
     assert tail.count("global_store_dwordx4") == 1, tail
     assert tail.count("global_store_dword") == 2, tail
@@ -138,4 +142,4 @@ def test_peft_walkers_do_not_spill(peft_asm):
         scratch = re.search(r"; ScratchSize: (\d+)", peft_asm[end:end + 4000])
         assert scratch and int(scratch.group(1)) == 0, f"{m.group(1)} spills: {scratch.group(0)}"
         found += 1
-    assert found == 4, found
+    assert found == 6, found

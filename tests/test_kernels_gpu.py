@@ -764,3 +764,94 @@ def test_vit_embed_ln_matches_separate(ops, dev, n, npch, D):
     assert rel(x0, x0r) < 1e-5
     assert rel(y, yr) < 4e-3
     assert rel(m1, x0r.mean(1)) < 1e-5
+
+
+# ------------------------------------------------- the image tower's half residual stream (x16)
+H16 = torch.float16
+
+
+@pytest.mark.parametrize("M,D,keep", [(4096 + 7, 768, 0.9), (1000, 512, 1.0), (50432, 768, 0.9)])
+def test_adapter_ln_fwd_x16(ops, dev, M, D, keep):
+    """lc_adapter_ln_fwd_x16 (resid and x_out in IEEE half, the reference's autocast residual
+    dtype) against the f32 kernel on the same half inputs: x_out is the f32 result rounded to
+    half, bit for bit (the same arithmetic, then one RNE rounding); h bit-identical; the
+    LayerNorm reads x_out as stored (statistics and y against torch fp32 on the half values)."""
+    torch.manual_seed(M + D)
+    z = torch.randn(M, D, device=dev).to(BF)
+    Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
+    Wu = (torch.randn(D, 64, device=dev) * 0.125).to(BF)
+    bd = torch.randn(64, device=dev) * 0.1
+    bu = torch.randn(D, device=dev) * 0.1
+    xh = (torch.randn(M, D, device=dev) * 2).to(H16)
+    gam, bet = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    seed = 777
+    xo1, h1 = torch.empty(M, D, device=dev), torch.empty(M, 64, device=dev, dtype=BF)
+    y1 = torch.empty(M, D, device=dev, dtype=BF)
+    m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, keep, seed, xh.float(), xo1, h1, gam, bet, y1, m1, r1)
+    xo2, h2 = torch.full((M, D), float("nan"), device=dev, dtype=H16), torch.empty_like(h1)
+    y2, m2, r2 = torch.empty_like(y1), torch.empty_like(m1), torch.empty_like(r1)
+    ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, keep, seed, xh, xo2, h2, gam, bet, y2, m2, r2)
+    assert torch.equal(h2, h1)
+    assert torch.equal(xo2, xo1.to(H16))
+    xr = xo2.float()
+    mu = xr.mean(1)
+    rs = torch.rsqrt(((xr - mu[:, None]) ** 2).mean(1) + 1e-5)
+    assert rel(m2, mu) < 1e-5 and rel(r2, rs) < 1e-5
+    assert rel(y2.float(), (xr - mu[:, None]) * rs[:, None] * gam + bet) < 4e-3
+    with pytest.raises(ValueError):  # one dtype for resid and x_out
+        ops.adapter_ln_fwd(z, Wd, bd, Wu, bu, 0.1, keep, seed, xh.float(), xo2, h2, gam, bet, y2,
+                           m2, r2)
+
+
+@pytest.mark.parametrize("n,npch,D", [(3, 196, 768), (5, 49, 512), (256, 196, 768)])
+def test_vit_embed_ln_x16(ops, dev, n, npch, D):
+    """lc_vit_embed_ln_x16: x0 is the f32 kernel's x0 rounded to half, bit for bit, and the first
+    ln_1 reads x0 as stored (against torch fp32 on the half x0)."""
+    torch.manual_seed(n + D + 1)
+    L = npch + 1
+    pe = torch.randn(n * npch, D, device=dev)
+    cls, pos = torch.randn(D, device=dev), torch.randn(L, D, device=dev) * 0.1
+    gp, bp = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    g1, b1 = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    x0f, y = torch.empty(n * L, D, device=dev), torch.empty(n * L, D, device=dev, dtype=BF)
+    m1, r1 = torch.empty(n * L, device=dev), torch.empty(n * L, device=dev)
+    ops.vit_embed_ln(pe, cls, pos, gp, bp, g1, b1, x0f, y, m1, r1, n, npch)
+    x0h = torch.empty(n * L, D, device=dev, dtype=H16)
+    yh = torch.empty_like(y)
+    m1h, r1h = torch.empty_like(m1), torch.empty_like(r1)
+    ops.vit_embed_ln(pe, cls, pos, gp, bp, g1, b1, x0h, yh, m1h, r1h, n, npch)
+    assert torch.equal(x0h, x0f.to(H16))
+    yr = torch.nn.functional.layer_norm(x0h.float(), (D,), g1, b1, 1e-5)
+    assert rel(yh.float(), yr) < 4e-3
+    xr = x0h.float()
+    mu = xr.mean(1)
+    assert rel(m1h, mu) < 1e-5
+    assert rel(r1h, torch.rsqrt(((xr - mu[:, None]) ** 2).mean(1) + 1e-5)) < 1e-5
+
+
+@pytest.mark.parametrize("D", [768, 512, 64])
+def test_layernorm_x16(ops, dev, D):
+    """LayerNorm forward (plain and row-gathered, as ln_post) and backward reading a half x:
+    equal to the f32 kernels on x.float() (the same arithmetic on the same values)."""
+    torch.manual_seed(D)
+    M = 3000
+    xh = (torch.randn(M, D, device=dev) * 3).to(H16)
+    gam, bet = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    idx = torch.arange(0, M, 197, device=dev, dtype=torch.int32)
+    for rows, ri in ((M, None), (idx.numel(), idx)):
+        yf, yh = (torch.empty(rows, D, device=dev) for _ in range(2))
+        mf, rf, mh, rh = (torch.empty(rows, device=dev) for _ in range(4))
+        ops.layernorm_fwd(xh.float(), gam, bet, yf, mf, rf, row_idx=ri)
+        ops.layernorm_fwd(xh, gam, bet, yh, mh, rh, row_idx=ri)
+        assert torch.equal(yh, yf) and torch.equal(mh, mf) and torch.equal(rh, rf)
+        dy = torch.randn(rows, D, device=dev).to(BF)
+        dres = torch.randn(M, D, device=dev)
+        outs = []
+        for x in (xh.float(), xh):
+            dx = dres.clone() * 0
+            dxb = torch.zeros(M, D, device=dev, dtype=BF)
+            ops.layernorm_bwd(dy, x, mf, rf, gam, dx, dxb, dres=dres if ri is None else None,
+                              row_idx=ri)
+            outs.append((dx, dxb))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
