@@ -187,6 +187,20 @@ int lc_vit_embed_ln_x16(hipStream_t stream, int n_img, int n_patch, int D, const
                         const float* cls, const float* pos, const float* ln_pre_w,
                         const float* ln_pre_b, void* x0, const float* ln1_w, const float* ln1_b,
                         void* y, float* mean1, float* rstd1);
+/* lc_layernorm_bwd_x16 with the residual gradient in IEEE half as well: dres and dx half
+ * [rows, ldo] (ldo % 4 == 0, 8-B aligned), the gradient carrying a power-of-two scale set
+ * upstream (lc_grad_pow2_normalize: the reference's GradScaler, methods/adapter_clip.py:93);
+ * dx_bf16 is the bf16 copy of the stored half value. */
+int lc_layernorm_bwd_g16(hipStream_t stream, int rows, int D, const void* dy, int dy_f32,
+                         long ldy, const void* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const void* dres, void* dx, void* dx_bf16,
+                         long ldo, const int* row_idx);
+/* lc_adapter_wgrad_ws whose results are divided by *gscale (device f32: the power-of-two scale
+ * gout / dpre carry; exact), so the scaled backward's weight gradients land unscaled. */
+int lc_adapter_wgrad_ws_unscaled(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                                 const void* h, const void* z, long ldz, const void* dpre,
+                                 float scale, float* dWu, float* dbu, float* dWd, float* dbd,
+                                 void* ws, long ws_bytes, const float* gscale);
 int lc_adapter_ln_fwd_x16(hipStream_t stream, int M, int D, const void* z, long ldz,
                           const void* Wd, const float* bd, const void* Wu, const float* bu,
                           float scale, float keep, unsigned long long seed,

@@ -1546,7 +1546,10 @@ struct TnProb {
   float* part;        // two-stage mode: one partial slot per workgroup (tn_reduce_kernel sums
                       // them into C / the column sums); nullptr: f32 atomics into C
   int pw;             // W panel width of the launch (128 or 256)
+  const float* div;   // optional device scalar every result is divided by (a power-of-two
+                      // gradient scale: exact), or nullptr
 };
+LC_DEV float tn_unscale(const TnProb& p, float v) { return p.div ? v / *p.div : v; }
 
 // Geometry of the wide x skinny reduction for a W panel of PW columns (128 or 256; 256 halves
 // the re-reads of S, one per panel, for the adapter's D = 768: 3 panels instead of 6).
@@ -1722,17 +1725,17 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
         const int j = wsv * 32 + jj * 16 + t;
         if (j < p.ns) {
           float* dst = p.trans ? p.C + (long)j * p.ldc + n : p.C + (long)n * p.ldc + j;
-          atomicAdd(dst, acc[i][jj][r] * p.alpha);
+          atomicAdd(dst, tn_unscale(p, acc[i][jj][r] * p.alpha));
         }
       }
-      if (do_csw && t == 0) atomicAdd(p.cs_w + n, csw[i][r] * p.cs_w_scale);
+      if (do_csw && t == 0) atomicAdd(p.cs_w + n, tn_unscale(p, csw[i][r] * p.cs_w_scale));
     }
   if (do_css && g == 0) {
     // css[jj]: lane holds sum_k S[k][32wsv + 16jj + t] in every r
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wsv * 32 + jj * 16 + t;
-      if (j < p.ns) atomicAdd(p.cs_s + j, css[jj][0] * p.cs_s_scale);
+      if (j < p.ns) atomicAdd(p.cs_s + j, tn_unscale(p, css[jj][0] * p.cs_s_scale));
     }
   }
 }
@@ -1772,17 +1775,17 @@ tn_reduce_kernel(TnProb p0, TnProb p1) {
       const int tile = n / pw, nl = n % pw;
       const float v = sum_slots(p.part + (long)tile * p.n_chunks * ps + nl * 64 + j, p.n_chunks, ps);
       float* dst = p.trans ? p.C + (long)j * p.ldc + n : p.C + (long)n * p.ldc + j;
-      *dst += v * p.alpha;
+      *dst += tn_unscale(p, v * p.alpha);
     } else if (k < p.Nw * 64 + p.Nw) {  // column sums of W
       if (!p.cs_w) continue;
       const int n = k - p.Nw * 64, tile = n / pw, nl = n % pw;
       const float v = sum_slots(p.part + (long)tile * p.n_chunks * ps + pw * 64 + nl, p.n_chunks, ps);
-      p.cs_w[n] += v * p.cs_w_scale;
+      p.cs_w[n] += tn_unscale(p, v * p.cs_w_scale);
     } else {  // column sums of S (tile 0's walkers carry them)
       const int j = k - p.Nw * 64 - p.Nw;
       if (!p.cs_s || j >= p.ns) continue;
       const float v = sum_slots(p.part + pw * 64 + pw + j, p.n_chunks, ps);
-      p.cs_s[j] += v * p.cs_s_scale;
+      p.cs_s[j] += tn_unscale(p, v * p.cs_s_scale);
     }
   }
 }
@@ -2309,13 +2312,15 @@ int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ld
                              nullptr, 0);
 }
 
-int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long ldg,
-                        const void* h, const void* z, long ldz, const void* dpre, float scale,
-                        float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes) {
+static int adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                         const void* h, const void* z, long ldz, const void* dpre, float scale,
+                         float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes,
+                         const float* div) {
   LC_CHECK_ARG(M > 0 && D > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0 && ldg >= D &&
                ldz >= D);
   LC_CHECK_ARG(dWu != nullptr && dWd != nullptr);
   TnProb up{}, down{};
+  up.div = down.div = div;
   // dWu[D][64] += scale * gout^T h ; dbu += scale * colsum(gout)
   up.W = static_cast<const bf16_t*>(gout);
   up.ldw = ldg;
@@ -2375,5 +2380,23 @@ int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long
   }
   LC_LAUNCH_RET();
 }
+
+int lc_adapter_wgrad_ws(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                        const void* h, const void* z, long ldz, const void* dpre, float scale,
+                        float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes) {
+  return adapter_wgrad(stream, M, D, gout, ldg, h, z, ldz, dpre, scale, dWu, dbu, dWd, dbd, ws,
+                       ws_bytes, nullptr);
+}
+
+#ifndef LC_F16
+int lc_adapter_wgrad_ws_unscaled(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                                 const void* h, const void* z, long ldz, const void* dpre,
+                                 float scale, float* dWu, float* dbu, float* dWd, float* dbd,
+                                 void* ws, long ws_bytes, const float* gscale) {
+  LC_CHECK_ARG(gscale != nullptr);
+  return adapter_wgrad(stream, M, D, gout, ldg, h, z, ldz, dpre, scale, dWu, dbu, dWd, dbd, ws,
+                       ws_bytes, gscale);
+}
+#endif
 
 }  // extern "C"

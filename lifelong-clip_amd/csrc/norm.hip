@@ -183,12 +183,14 @@ ln_fwd_kernel(int rows, const XT* __restrict__ x, long ldx, const int* __restric
 }
 
 // dx = rstd * (g - mean(g) - xhat * mean(g * xhat)), g = dy * gamma; total = dres + dx.
-template <int V, typename XT = float>
+// XT: x's element type; GT: the residual gradient's (dres in, dx out): float, or _Float16 (the
+// half residual stream's gradient, scaled by a power of two upstream)
+template <int V, typename XT = float, typename GT = float>
 __global__ void __launch_bounds__(256)
 ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
               const XT* __restrict__ x, long ldx, const float* __restrict__ mean,
               const float* __restrict__ rstd, const float* __restrict__ gamma,
-              const float* __restrict__ dres, float* __restrict__ dx, bf16_t* __restrict__ dxb,
+              const GT* __restrict__ dres, GT* __restrict__ dx, bf16_t* __restrict__ dxb,
               long ldo, const int* __restrict__ row_idx, uint8_t* __restrict__ qo, long ldq,
               uint8_t* __restrict__ q_scale, long q_rows) {
   constexpr int D = V * 64;
@@ -204,7 +206,7 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
   load_row_f32<V>(gamma, lane, gm);
   // the residual gradient too, before the reductions (it was a second exposed round trip)
   float r[V];
-  if (dres) load_row_f32<V>(dres + xr * ldo, lane, r);
+  if (dres) load_row_x<V, GT>(dres + xr * ldo, lane, r);
   const float mu = mean[row], rs = rstd[row];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -223,7 +225,11 @@ ln_bwd_kernel(int rows, const void* __restrict__ dy, int dy_f32, long ldy,
 #pragma unroll
     for (int i = 0; i < V; ++i) out[i] += r[i];
   }
-  store_row_f32<V>(dx + xr * ldo, lane, out);
+  if constexpr (sizeof(GT) == 2) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) out[i] = xround<GT>(out[i]);  // the bf16 copy of the stored value
+  }
+  store_row_x<V, GT>(dx + xr * ldo, lane, out);
   if (dxb) store_row_bf16<V>(dxb + xr * ldo, lane, out);
   // the bf16 result also as the next fp8 GEMM's operand (the codes of dxb + quant_fp8)
   if constexpr (V % 4 == 0)
@@ -367,24 +373,30 @@ int grid_for(long work, int block) {
 
 // x16: x (the forward's LayerNorm input, the residual stream) is IEEE half
 int ln_bwd(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy, const void* x,
-           long ldx, const float* mean, const float* rstd, const float* gamma, const float* dres,
-           float* dx, void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
-           void* q_scale, long q_rows, int x16 = 0) {
+           long ldx, const float* mean, const float* rstd, const float* gamma, const void* dres,
+           void* dx, void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
+           void* q_scale, long q_rows, int x16 = 0, int g16 = 0) {
   LC_CHECK_ARG(rows >= 0 && D % 64 == 0 && D >= 64 && D <= 1024);
   if (rows == 0) return LC_OK;
   dim3 grid((rows + 3) / 4), block(256);
   switch (D / 64) {
 #define LC_LN_B(V)                                                                              \
   case V:                                                                                      \
-    if (x16)                                                                                   \
+    if (g16)                                                                                   \
+      hipLaunchKernelGGL((ln_bwd_kernel<V, _Float16, _Float16>), grid, block, 0, st, rows, dy, \
+                         dy_f32, ldy, (const _Float16*)x, ldx, mean, rstd, gamma,              \
+                         (const _Float16*)dres, (_Float16*)dx, (bf16_t*)dx_bf16, ldo, row_idx,  \
+                         (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);                          \
+    else if (x16)                                                                              \
       hipLaunchKernelGGL((ln_bwd_kernel<V, _Float16>), grid, block, 0, st, rows, dy, dy_f32,   \
-                         ldy, (const _Float16*)x, ldx, mean, rstd, gamma, dres, dx,            \
-                         (bf16_t*)dx_bf16, ldo, row_idx, (uint8_t*)q, ldq, (uint8_t*)q_scale,   \
-                         q_rows);                                                               \
+                         ldy, (const _Float16*)x, ldx, mean, rstd, gamma, (const float*)dres,  \
+                         (float*)dx, (bf16_t*)dx_bf16, ldo, row_idx, (uint8_t*)q, ldq,          \
+                         (uint8_t*)q_scale, q_rows);                                            \
     else                                                                                       \
       hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, block, 0, st, rows, dy, dy_f32, ldy,          \
-                         (const float*)x, ldx, mean, rstd, gamma, dres, dx, (bf16_t*)dx_bf16,   \
-                         ldo, row_idx, (uint8_t*)q, ldq, (uint8_t*)q_scale, q_rows);            \
+                         (const float*)x, ldx, mean, rstd, gamma, (const float*)dres,          \
+                         (float*)dx, (bf16_t*)dx_bf16, ldo, row_idx, (uint8_t*)q, ldq,          \
+                         (uint8_t*)q_scale, q_rows);                                            \
     break;
     LC_LN_B(1) LC_LN_B(2) LC_LN_B(4) LC_LN_B(8) LC_LN_B(12) LC_LN_B(16)
     default:
@@ -466,6 +478,16 @@ int lc_layernorm_bwd_x16(hipStream_t st, int rows, int D, const void* dy, int dy
   LC_CHECK_ARG(x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0);
   return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
                 row_idx, nullptr, 0, nullptr, 0, 1);
+}
+
+int lc_layernorm_bwd_g16(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,
+                         const void* x, long ldx, const float* mean, const float* rstd,
+                         const float* gamma, const void* dres, void* dx, void* dx_bf16, long ldo,
+                         const int* row_idx) {
+  LC_CHECK_ARG(x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0 && ldo % 4 == 0 &&
+               ((uintptr_t)dx & 7) == 0 && ((uintptr_t)dres & 7) == 0);
+  return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
+                row_idx, nullptr, 0, nullptr, 0, 1, 1);
 }
 #endif
 

@@ -417,7 +417,7 @@ class BlockStack:
     # ------------------------------------------------------------------ backward
     def backward(self, saved, dx, dxb, grads, n_seq: int, L: int, on_layer=None,
                  grad_stream=None, need_dx: bool = True, prompt_grads=None,
-                 keep_input: bool = False):
+                 keep_input: bool = False, gscale=None):
         """dx f32 / dxb bf16 [rows, D]: gradient w.r.t. the stack output. grads: dict
         param -> f32 tensor (accumulated). on_layer(li) is called once layer li's PEFT gradients
         have been launched (layers run last to first). Returns (dx, dxb) w.r.t. the stack input.
@@ -440,8 +440,17 @@ class BlockStack:
         which then stops: zeroed below that layer).
 
         keep_input: never write into (dx, dxb) (a caller-kept buffer, ImageTower._grad_in); the
-        layers' output gradients then ping-pong between two other pairs."""
+        layers' output gradients then ping-pong between two other pairs.
+
+        dx float16 (the half residual stream's gradient, the fused adapter tower): every residual
+        gradient is stored in half, carrying the power-of-two scale `gscale` (device f32 [1],
+        set by the caller: ops.grad_pow2_normalize) that the weight gradients divide out."""
         M, D = dx.shape
+        gdt = dx.dtype
+        if gdt != F32 and (gscale is None or prompt_grads is not None
+                           or any(s.get("P", 0) or "R" in s for s in saved)):
+            raise ValueError("a half residual gradient needs its gscale and no prompt rows")
+        self._gscale = gscale
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
         ev = None
@@ -457,13 +466,13 @@ class BlockStack:
         dO = _empty((Mmax, D), self.dt, dev)
         dqkv = _empty((Mmax, 3 * D), self.dt, dev)
         dz = _empty((Mmax, D), self.dt, dev) if self.variant == "adapter" else None
-        dx_mid = _empty((Mmax, D), F32, dev)
+        dx_mid = _empty((Mmax, D), gdt, dev)
         dx_midb = _empty((Mmax, D), self.dt, dev)
         # output-gradient buffers: the incoming pair and one more (ping-pong); prompt layers
         # expand the current gradient into a free pair and compact their output back
-        pairs = [(dx, dxb), (_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev))]
+        pairs = [(dx, dxb), (_empty((Mmax, D), gdt, dev), _empty((Mmax, D), self.dt, dev))]
         if keep_input:
-            pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
+            pairs.append((_empty((Mmax, D), gdt, dev), _empty((Mmax, D), self.dt, dev)))
         cur = 0
         # fp8 (no adapter: the block output gradient feeds c_proj dX directly): ln_1's backward
         # also writes its result as the fp8 operand of the next (lower) block's c_proj dX GEMM
@@ -569,6 +578,7 @@ class BlockStack:
             else:
                 cur = out
         self.sync_grads()
+        self._gscale = None
         if not need_dx:
             return None, None
         return pairs[cur][0][:M], pairs[cur][1][:M]
@@ -616,7 +626,8 @@ class BlockStack:
             ops.adapter_wgrad(gout, h, z, dpre, ad.scale, self._grad(grads, ad.up_proj.weight),
                               self._grad(grads, ad.up_proj.bias),
                               self._grad(grads, ad.down_proj.weight),
-                              self._grad(grads, ad.down_proj.bias))
+                              self._grad(grads, ad.down_proj.bias),
+                              gscale=getattr(self, "_gscale", None))
         return dz
 
     # LCCLIP_MERGE_BATCH=0: one lc_merge_weight launch per LoRA merge / cast (A/B experiments)
@@ -667,15 +678,17 @@ class RowGrad:
         self.prev = None       # int64 rows written by the previous use
         self.prev_key = None
 
-    def get(self, rows, D, dev, idx, key=None, dt=BF16):
+    def get(self, rows, D, dev, idx, key=None, dt=BF16, gdt=F32):
+        """dt: the 16-bit copy's type; gdt: the gradient's (f32, or float16 for the half
+        residual stream)."""
         b = self.buf
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
             # graph-pool memory: fresh zeros, captured as part of the graph, not kept
-            return (torch.zeros((rows, D), dtype=F32, device=dev),
+            return (torch.zeros((rows, D), dtype=gdt, device=dev),
                     torch.zeros((rows, D), dtype=dt, device=dev))
         if (b is None or b[0].shape[0] < rows or b[0].shape[1] != D or b[0].device != dev
-                or b[1].dtype != dt):
-            self.buf = b = (torch.zeros((rows, D), dtype=F32, device=dev),
+                or b[1].dtype != dt or b[0].dtype != gdt):
+            self.buf = b = (torch.zeros((rows, D), dtype=gdt, device=dev),
                             torch.zeros((rows, D), dtype=dt, device=dev))
         elif self.prev is not None and (key is None or key != self.prev_key):
             for t in b:
@@ -692,6 +705,7 @@ class ImageTower:
         self.stack = stack
         self._key = None
         self._grad_in = RowGrad()  # ln_post's backward writes the CLS rows only
+        self._gsc = None  # the half residual gradient's scale (device f32 [1])
 
     def _stage(self):
         v = self.visual
@@ -810,6 +824,7 @@ class ImageTower:
     # fused adapter tower: lc_*_x16): a third less HBM traffic in the fused adapter + LayerNorm
     # forward and the x read of every LayerNorm backward. False: the f32 stream (A/Bs)
     RESID16 = True
+    GRAD_EXP = 12  # the half residual gradient's scale target, 2^GRAD_EXP <= max|dL/df| s < 2^13
 
     def _resid16(self):
         st = self.stack
@@ -864,17 +879,30 @@ class ImageTower:
         dev = df.device
         n, L = ctx["n"], ctx["L"]
         D = v.width
+        half = ctx["x"].dtype == F16  # the half residual stream: its gradient in half as well
+        gsc = None
+        if half:
+            # a per-call power-of-two gradient scale (the reference's GradScaler,
+            # methods/adapter_clip.py:93): max|dL/df| lands in [2^12, 2^13), which keeps the
+            # residual gradient (measured at <= 0.45 max|dL/df|, median 1e-4 of it) inside
+            # half's normal range; the weight gradients divide it out
+            df = df.contiguous().float().clone()
+            if self._gsc is None or self._gsc.device != dev:
+                self._gsc = torch.ones(1, dtype=F32, device=dev)
+            gsc = self._gsc
+            ops.grad_pow2_normalize(df, gsc, target_exp=self.GRAD_EXP)
         dfb = _empty(df.shape, BF16, dev)
         ops.cast_bf16(df.contiguous(), dfb)
         dln = _empty((n, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
-        dx, dxb = self._grad_in.get(n * L, D, dev, ctx["cls_idx"], key=(n, L))
+        dx, dxb = self._grad_in.get(n * L, D, dev, ctx["cls_idx"], key=(n, L),
+                                    gdt=F16 if half else F32)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
                                     need_dx=need_dx or 0 in ctx["prompt_layers"],
-                                    prompt_grads=prompt_grads, keep_input=True)
+                                    prompt_grads=prompt_grads, keep_input=True, gscale=gsc)
         return gx if need_dx else None
 
 

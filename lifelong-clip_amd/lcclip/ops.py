@@ -217,10 +217,20 @@ def layernorm_fwd_fp8(x, weight, bias, q, mean=None, rstd=None, y=None):
 
 
 def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_idx=None):
-    """x: the forward's input, f32 or float16 (the half residual stream)."""
+    """x: the forward's input, f32 or float16 (the half residual stream); dx (and dres): f32, or
+    float16 with a half x (the half residual stream's gradient, lc_layernorm_bwd_g16)."""
     rows = dy.shape[0]
     D = x.shape[1]
-    call(_x16("lc_layernorm_bwd", x, dy, dx_bf16), stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+    name = _x16("lc_layernorm_bwd", x, dy, dx_bf16)
+    if dx.dtype == F16:
+        if x.dtype != F16 or (dres is not None and dres.dtype != F16) or dx.stride(0) % 4 \
+                or dx.data_ptr() % 8 or (dres is not None and dres.stride(0) != dx.stride(0)):
+            raise ValueError("layernorm_bwd: a half gradient takes a half x and a half dres of "
+                             "dx's row stride (% 4), 8-B aligned")
+        name = "lc_layernorm_bwd_g16"
+    elif dres is not None and dres.dtype != F32:
+        raise TypeError("layernorm_bwd: dres must have dx's dtype")
+    call(name, stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
          dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
          ptr(dx_bf16), dx.stride(0), ptr(row_idx))
     return dx
@@ -460,8 +470,10 @@ def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
          dz.stride(0) if dz is not None else D)
 
 
-def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
-    """dWu += scale gout^T h, dbu += scale colsum(gout), dWd += dpre^T z, dbd += colsum(dpre)."""
+def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd, gscale=None):
+    """dWu += scale gout^T h, dbu += scale colsum(gout), dWd += dpre^T z, dbd += colsum(dpre).
+    gscale: optional device f32 scalar (a power-of-two gradient scale that gout / dpre carry):
+    every result is divided by it (lc_adapter_wgrad_ws_unscaled)."""
     M, D = gout.shape
     for t, name in ((gout, "gout"), (z, "z")):
         _rowmajor(t, HALF, name)
@@ -476,6 +488,13 @@ def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd):
     # two-stage reduction through the launch stream's split-K workspace (partials after its
     # ticket region; the stream orders every user of that buffer)
     ws = splitk_workspace(torch.cuda.current_stream(gout.device))
+    if gscale is not None:
+        if gout.dtype != BF16 or gscale.dtype != F32 or gscale.numel() != 1:
+            raise TypeError("adapter_wgrad: gscale takes bf16 operands and an f32 device scalar")
+        call("lc_adapter_wgrad_ws_unscaled", stream_of(gout), M, D, ptr(gout), gout.stride(0),
+             ptr(h), ptr(z), z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd),
+             ptr(dbd), ptr(ws), ws.numel(), ptr(gscale))
+        return
     call(_sym16("lc_adapter_wgrad_ws", gout, h, z, dpre), stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
          z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd), ptr(ws),
          ws.numel())

@@ -114,19 +114,36 @@ class _GradRound(torch.autograd.Function):
 
 class _GradScaleSet(torch.autograd.Function):
     """Identity forward; in backward sets the hook's gradient scale from the incoming gradient,
-    s = 2^(10 - floor(log2 max|g|)) (the IEEE-half text tower's per-call loss scale,
-    ops.grad_pow2_normalize / head.hip), before any rounding inside the tower runs."""
+    s = 2^(e - floor(log2 max|g|)) (the per-call loss scale of the IEEE-half text tower, e = 10,
+    and of the image tower's half residual gradient, e = 12: ops.grad_pow2_normalize /
+    head.hip), before any rounding inside the tower runs."""
 
     @staticmethod
-    def forward(ctx, x, hook):
-        ctx.hook = hook
+    def forward(ctx, x, hook, e=10):
+        ctx.hook, ctx.e = hook, e
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
         a = g.abs().max().item()
-        ctx.hook.gs = 2.0 ** (10 - math.floor(math.log2(a))) if 0 < a < float("inf") else 1.0
-        return g, None
+        ctx.hook.gs = 2.0 ** (ctx.e - math.floor(math.log2(a))) if 0 < a < float("inf") else 1.0
+        return g, None, None
+
+
+class _ResidRound(torch.autograd.Function):
+    """The half residual stream of the MI355X image tower (ImageTower.RESID16): x rounded to
+    IEEE half; its gradient stored in half too, carrying the hook's power-of-two scale gs
+    (lcclip ImageTower.backward: ops.grad_pow2_normalize, target 2^12; lc_layernorm_bwd_g16)."""
+
+    @staticmethod
+    def forward(ctx, x, hook):
+        ctx.hook = hook
+        return _hf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        s = ctx.hook.gs
+        return _hf(g * s) / s, None
 
 
 class _QuickGeluRound(torch.autograd.Function):
@@ -210,6 +227,9 @@ class Rounding:
                 q, k, v, scale, causal, self._rnd, self._grnd)
             if kind == "f16":
                 self.top = lambda x: _GradScaleSet.apply(x, self)
+            else:  # the image tower: its half residual gradient's scale (bf16 roundings ignore it)
+                self.top = lambda x: _GradScaleSet.apply(x, self, 12)
+                self.resid = lambda x: _ResidRound.apply(x, self)
 
     def __call__(self, x):
         r = self._rnd(x.detach())

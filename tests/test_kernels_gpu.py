@@ -855,3 +855,60 @@ def test_layernorm_x16(ops, dev, D):
                               row_idx=ri)
             outs.append((dx, dxb))
         assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("D", [768, 512, 64])
+def test_layernorm_bwd_g16(ops, dev, D):
+    """LayerNorm backward with the residual gradient in half (dres in, dx out, lc_layernorm_bwd_g16):
+    dx is the f32 kernel's result (on dres.float()) rounded to half, bit for bit, and the bf16
+    copy is that half value rounded to bf16."""
+    torch.manual_seed(D + 5)
+    M = 2000
+    xh = (torch.randn(M, D, device=dev) * 3).to(H16)
+    gam, bet = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    y, mu, rs = torch.empty(M, D, device=dev, dtype=BF), torch.empty(M, device=dev), torch.empty(M, device=dev)
+    ops.layernorm_fwd(xh, gam, bet, y, mu, rs)
+    dy = (torch.randn(M, D, device=dev) * 100).to(BF)
+    dres = (torch.randn(M, D, device=dev) * 50).to(H16)
+    dx32, dxb32 = torch.empty(M, D, device=dev), torch.empty(M, D, device=dev, dtype=BF)
+    ops.layernorm_bwd(dy, xh, mu, rs, gam, dx32, dxb32, dres=dres.float())
+    dx16 = torch.full((M, D), float("nan"), device=dev, dtype=H16)
+    dxb16 = torch.empty_like(dxb32)
+    ops.layernorm_bwd(dy, xh, mu, rs, gam, dx16, dxb16, dres=dres)
+    assert torch.equal(dx16, dx32.to(H16))
+    assert torch.equal(dxb16, dx16.float().to(BF))
+    # row-gathered, no dres (ln_post's backward into the CLS rows)
+    idx = torch.arange(0, M, 197, device=dev, dtype=torch.int32)
+    dl = torch.randn(idx.numel(), D, device=dev) * 10
+    g32, g16 = torch.zeros(M, D, device=dev), torch.zeros(M, D, device=dev, dtype=H16)
+    b32, b16 = (torch.zeros(M, D, device=dev, dtype=BF) for _ in range(2))
+    ops.layernorm_bwd(dl, xh, mu[idx.long()], rs[idx.long()], gam, g32, b32, row_idx=idx)
+    ops.layernorm_bwd(dl, xh, mu[idx.long()], rs[idx.long()], gam, g16, b16, row_idx=idx)
+    assert torch.equal(g16, g32.to(H16))
+    with pytest.raises(ValueError):  # a half gradient needs a half x
+        ops.layernorm_bwd(dy, xh.float(), mu, rs, gam, dx16, dxb16, dres=dres)
+
+
+def test_adapter_wgrad_unscaled(ops, dev):
+    """lc_adapter_wgrad_ws_unscaled divides every weight / bias gradient by the device scale
+    (a power of two: exactly the unscaled launch's result on unscaled operands)."""
+    torch.manual_seed(9)
+    M, D = 50432 // 8, 768
+    s = 2.0 ** 13
+    g = torch.randn(M, D, device=dev).to(BF)
+    h = torch.randn(M, 64, device=dev).to(BF)
+    z = torch.randn(M, D, device=dev).to(BF)
+    dp = torch.randn(M, 64, device=dev).to(BF)
+    outs = []
+    for scaled in (False, True):
+        bufs = [torch.zeros(D, 64, device=dev), torch.zeros(D, device=dev),
+                torch.zeros(64, D, device=dev), torch.zeros(64, device=dev)]
+        if scaled:
+            gs = torch.full((1,), s, device=dev)
+            ops.adapter_wgrad((g.float() * s).to(BF), h, z, (dp.float() * s).to(BF), 0.1, *bufs,
+                              gscale=gs)
+        else:
+            ops.adapter_wgrad(g, h, z, dp, 0.1, *bufs)
+        outs.append(bufs)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
