@@ -43,6 +43,8 @@ extern "C" {
  * of the bf16-rounded result, bit-identical to the bf16 epilogue followed by lc_quant_fp8 */
 #define LC_EPI_GELU_D_Q8 12 /* out0 bf16 = QuickGELU'(pre); out1 fp8 = QuickGELU(pre)          */
 #define LC_EPI_MUL_Q8 13    /* out1 fp8 = alpha*acc * aux_bf16 (out0 unused)                   */
+/* the image tower's half residual stream (see the _x16 entry points below) */
+#define LC_EPI_RESID16 14   /* out0 half = aux_half + alpha*acc + bias  (x + sublayer(x))      */
 
 /* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue; A, B bf16, K % 64 == 0, N % 64 == 0,
  * lda / ldb (elements) multiples of 8 and below 2^22, ldo0 / ldo1 below 2^21 (the kernels address

@@ -41,6 +41,8 @@ enum {
   // epilogue followed by quant_fp8 (quant.hip) — the next fp8 GEMM's A operand straight from here
   EPI_GELU_D_Q8 = 12,  // out0 bf16 = quick_gelu'(pre) ; out1 fp8 = quick_gelu(pre), pre = acc+bias
   EPI_MUL_Q8 = 13,     // out1 fp8 = (acc*alpha) * aux_bf16 (out0 unused)
+  // the half residual stream (lc_common.h xres): out0 half = aux_half + acc*alpha + bias
+  EPI_RESID16 = 14,
 };
 
 namespace {
@@ -149,7 +151,7 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
   // issued after them would wait for their acknowledgement.
   constexpr bool AUXF = (EPI == EPI_RESID || EPI == EPI_AD_UP);
   constexpr bool AUXB = (EPI == EPI_GELU_BWD || EPI == EPI_MUL || EPI == EPI_AD_MASK ||
-                         EPI == EPI_AD_ADD || EPI == EPI_MUL_Q8);
+                         EPI == EPI_AD_ADD || EPI == EPI_MUL_Q8 || EPI == EPI_RESID16);
   constexpr bool AUX2 = (EPI == EPI_AD_UP);
   constexpr int NIT = PASS / RPI;
   float pf_f[2][NIT][CPL];
@@ -246,8 +248,9 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
       ep.q_scale[fp8_scale_index(m, n >> 5, ep.q_rows)] = (uint8_t)byte;
     }
   };
-  // bf16 element i of a lane's packed side input
+  // bf16 element i of a lane's packed side input (hfv: IEEE half, the half residual stream)
   auto bfv = [](const uint32_t* x, int i) { return bf2f((i & 1) ? (x[i >> 1] >> 16) : (x[i >> 1] & 0xffff)); };
+  auto hfv = [](const uint32_t* x, int i) { return h2f((i & 1) ? (x[i >> 1] >> 16) : (x[i >> 1] & 0xffff)); };
   if constexpr (AUXF || AUXB) prefetch(0, 0);
   uint64_t seed = ep.seed;
   if constexpr (EPI == EPI_AD_DOWN)
@@ -288,6 +291,14 @@ LC_DEV void store_tile(f32x4 (&acc)[TM][TN], char* smem, int smem_bytes, int m0,
 #pragma unroll
         for (int i = 0; i < CPL; ++i) w[i] = xf[i] + v[i];
         store_f(rs0, ldo0, m, w);
+      } else if constexpr (EPI == EPI_RESID16) {
+        static_assert(CPL == 8, "8 halves (16 B) per lane");
+#pragma unroll
+        for (int i = 0; i < CPL; ++i) w[i] = hfv(xb, i) + v[i];
+        // temporal: the next LayerNorm reads it at once, the backward later
+        __builtin_amdgcn_raw_buffer_store_b128(
+            lc_u32x4{pack2h(w[0], w[1]), pack2h(w[2], w[3]), pack2h(w[4], w[5]), pack2h(w[6], w[7])},
+            rs0, (int)(((m - m0) * ldo0 + n) * 2), 0, 0);
       } else if constexpr (EPI == EPI_GELU) {
         store_bf(rs0, ldo0, m, v);
 #pragma unroll
@@ -1828,6 +1839,7 @@ int launch_nt(hipStream_t st, int epi, int M, int N, int K, const bf16_t* A, lon
     LC_NT_CASE(EPI_BF16)
     LC_NT_CASE(EPI_F32)
     LC_NT_CASE(EPI_RESID)
+    LC_NT_CASE(EPI_RESID16)
     LC_NT_CASE(EPI_GELU)
     LC_NT_CASE(EPI_GELU_BWD)
     LC_NT_CASE(EPI_BF16_F32)
@@ -2046,6 +2058,7 @@ int launch_g8(hipStream_t st, int epi, int M, int N, int K, const void* A, long 
     LC_G8_CASE(EPI_BF16)
     LC_G8_CASE(EPI_F32)
     LC_G8_CASE(EPI_RESID)
+    LC_G8_CASE(EPI_RESID16)
     LC_G8_CASE(EPI_GELU)
     LC_G8_CASE(EPI_GELU_D)
     LC_G8_CASE(EPI_MUL)
@@ -2081,7 +2094,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
   // x ldo x 4 B (f32 outputs) must stay below 2^31 (num_records and the int offsets)
   LC_CHECK_ARG(ldo0 < (1L << 21) && ldo1 < (1L << 21));
-  LC_CHECK_ARG(epi >= 0 && epi <= EPI_AD_ADD);
+  LC_CHECK_ARG((epi >= 0 && epi <= EPI_AD_ADD) || epi == EPI_RESID16);
   if (epi == EPI_GELU || epi == EPI_BF16_F32 || epi == EPI_GELU_D)
     LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
   if (epi == EPI_RESID || epi == EPI_GELU_BWD || epi == EPI_MUL || epi >= EPI_AD_UP)
@@ -2152,7 +2165,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
                        aux, ldaux, ep, ws, ws_bytes);
     case 8:
       if (epi != EPI_BF16 && epi != EPI_F32 && epi != EPI_RESID && epi != EPI_GELU &&
-          epi != EPI_GELU_D && epi != EPI_MUL)
+          epi != EPI_GELU_D && epi != EPI_MUL && epi != EPI_RESID16)
         return launch_pp(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1, ldo1,
                          aux, ldaux, ep, ws, ws_bytes);
       return launch_g8<false>(stream, epi, M, N, K, a, lda, b, ldb, bias, alpha, out0, ldo0, out1,
@@ -2179,7 +2192,7 @@ int lc_gemm_nt(hipStream_t stream, int epi, int M, int N, int K, const void* A, 
 int lc_gemm_nt_ws(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                   const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                   void* out1, long ldo1, const void* aux, long ldaux, void* ws, long ws_bytes) {
-  LC_CHECK_ARG(epi >= 0 && epi <= 7);
+  LC_CHECK_ARG((epi >= 0 && epi <= 7) || epi == EPI_RESID16);
   LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
   // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows
   // x ldo x 4 B (f32 outputs) must stay below 2^31 (num_records and the int offsets)
@@ -2205,7 +2218,8 @@ int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void*
                sb_rows >= N && sa_rows % 256 == 0 && sb_rows % 256 == 0);
   LC_CHECK_ARG(((uintptr_t)sa & 15) == 0 && ((uintptr_t)sb & 15) == 0);
   LC_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_RESID || epi == EPI_GELU ||
-               epi == EPI_GELU_D || epi == EPI_MUL || epi == EPI_GELU_D_Q8 || epi == EPI_MUL_Q8);
+               epi == EPI_GELU_D || epi == EPI_MUL || epi == EPI_GELU_D_Q8 || epi == EPI_MUL_Q8 ||
+               epi == EPI_RESID16);
   const bool q8 = epi == EPI_GELU_D_Q8 || epi == EPI_MUL_Q8;
   if (epi != EPI_MUL_Q8) LC_CHECK_ARG(out0 != nullptr && ldo0 % 8 == 0 && ldo0 >= N);
   if (epi == EPI_GELU || epi == EPI_GELU_D) LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 8 == 0);
@@ -2213,7 +2227,7 @@ int lc_gemm_nt_fp8(hipStream_t stream, int epi, int M, int N, int K, const void*
   if (q8)
     LC_CHECK_ARG(out1 != nullptr && ldo1 >= N && ldo1 % 16 == 0 && ((uintptr_t)out1 & 15) == 0 &&
                  q_scale != nullptr && q_rows >= (M + 255) / 256 * 256 && q_rows % 256 == 0);
-  if (epi == EPI_RESID || epi == EPI_MUL || epi == EPI_MUL_Q8)
+  if (epi == EPI_RESID || epi == EPI_MUL || epi == EPI_MUL_Q8 || epi == EPI_RESID16)
     LC_CHECK_ARG(aux != nullptr && ldaux >= N && ldaux % 8 == 0);
   LC_CHECK_ARG(ws == nullptr || (ws_bytes >= LC_SPLITK_TICKET_BYTES && ((uintptr_t)ws & 255) == 0));
   // the epilogue's buffer descriptors span one 256-row tile with 32-bit byte offsets: 256 rows

@@ -35,6 +35,7 @@ import torch
 
 from . import ops
 from .ops import BF16, F16, F32, EPI_BF16, EPI_F32, EPI_GELU, EPI_GELU_D, EPI_MUL, EPI_RESID
+from .ops import EPI_RESID16
 from .ops import EPI_GELU_D_Q8, EPI_MUL_Q8
 
 _seed_counter = itertools.count(1)
@@ -280,10 +281,13 @@ class BlockStack:
         # (ops.adapter_ln_fwd: ln_2 of the block, ln_1 of the next one); ln1_ready carries the
         # statistics of an ln_1 the previous block already wrote into tmp_h
         fuse_ln = (self.variant == "adapter" and q_h is None and D in (512, 768) and self.FUSE_LN)
-        if xdt != F32 and not (fuse_ln and q_g is None and last_ln is not None and not prompts
-                               and not replace and stop is None):
-            raise ValueError("a half residual stream runs the fused adapter tower only (no "
-                             "prompts, no fp8, the stack's closing LayerNorm fused: last_ln)")
+        if xdt != F32 and not (q_g is None and q_h is None and not prompts and not replace
+                               and stop is None and (
+                                   (fuse_ln and last_ln is not None) or self.variant == "lora")):
+            raise ValueError("a half residual stream runs the fused adapter tower (with its "
+                             "closing LayerNorm fused: last_ln) or the LoRA tower, bf16, without "
+                             "prompt rows")
+        e_resid = EPI_RESID16 if xdt == F16 else EPI_RESID
         ln1_ready = None
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
             if stop is not None and idx >= stop:
@@ -346,7 +350,7 @@ class BlockStack:
                     ln2_done = False
                 s.update(z1=z1, hd1=hd1, keep=keep)
             else:
-                ops.gemm_nt(O, st.wo, EPI_RESID, x_mid, bias=blk.attn.out_proj.bias, aux=x)
+                ops.gemm_nt(O, st.wo, e_resid, x_mid, bias=blk.attn.out_proj.bias, aux=x)
                 mean2 = _empty((Mx,), F32, dev)
                 rstd2 = _empty((Mx,), F32, dev)
                 ln2_done = False
@@ -402,7 +406,7 @@ class BlockStack:
                                     s["keep"], seed2, x_mid, x_out, hd2, seed_dev=self.seed_dev)
                 s.update(z2=z2, hd2=hd2)
             else:
-                wpr(EPI_RESID, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
+                wpr(e_resid, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
                          mean2=mean2, rstd2=rstd2, gd=pre, P=P)
@@ -828,8 +832,9 @@ class ImageTower:
 
     def _resid16(self):
         st = self.stack
-        return (self.RESID16 and self.FUSE_EMBED and st.variant == "adapter" and st.FUSE_LN
-                and st.precision == "bf16" and self.visual.width in (512, 768))
+        return (self.RESID16 and self.FUSE_EMBED and st.precision == "bf16"
+                and self.visual.width in (512, 768)
+                and ((st.variant == "adapter" and st.FUSE_LN) or st.variant == "lora"))
 
     def embed_ln1(self, img, half=False):
         """embed() and the first block's ln_1 in one launch (ops.vit_embed_ln): (x0, n, L,
@@ -853,7 +858,8 @@ class ImageTower:
         """forward() from a precomputed embed() (the MVP query and prompt passes share x0)."""
         self._stage()
         last = None
-        if x0.dtype == F16:  # ln_post fused into the last block's adapter over every row
+        if x0.dtype == F16 and self.stack.variant == "adapter":
+            # ln_post fused into the last block's adapter over every row
             v = self.visual
             M, D = x0.shape
             last = dict(w=v.ln_post.weight, b=v.ln_post.bias, y=_empty((M, D), BF16, x0.device),
@@ -879,7 +885,9 @@ class ImageTower:
         dev = df.device
         n, L = ctx["n"], ctx["L"]
         D = v.width
-        half = ctx["x"].dtype == F16  # the half residual stream: its gradient in half as well
+        # the adapter tower's half residual stream: its gradient in half as well (the LoRA
+        # tower keeps an f32 gradient: its rank-r weight gradients take no scale)
+        half = ctx["x"].dtype == F16 and self.stack.variant == "adapter"
         gsc = None
         if half:
             # a per-call power-of-two gradient scale (the reference's GradScaler,

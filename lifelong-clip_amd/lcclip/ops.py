@@ -12,6 +12,7 @@ F32 = torch.float32
 HALF = (BF16, F16)  # the 16-bit storage types (bf16: image tower; IEEE half: text tower)
 
 EPI_BF16, EPI_F32, EPI_RESID, EPI_GELU, EPI_GELU_BWD, EPI_BF16_F32, EPI_GELU_D, EPI_MUL = range(8)
+EPI_RESID16 = 14  # out0 / aux float16: the half residual stream (include/lc_clip.h)
 EPI_GELU_D_Q8, EPI_MUL_Q8 = 12, 13  # gemm_nt_fp8 only: the result as the next fp8 GEMM's operand
 
 
@@ -67,7 +68,14 @@ def gemm_nt(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None):
         raise ValueError("gemm_nt bias must be a contiguous f32 vector of length N")
     st = stream_of(A)
     ws = splitk_workspace(torch.cuda.current_stream(A.device)) if M >= 4096 else None
-    call(_sym16("lc_gemm_nt_ws", A, out0, out1, aux), st, epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
+    name = "lc_gemm_nt_ws"
+    if epi == EPI_RESID16:
+        if A.dtype != BF16 or out0.dtype != F16 or aux is None or aux.dtype != F16 \
+                or out0.stride(0) % 8 or aux.stride(0) % 8:
+            raise TypeError("gemm_nt EPI_RESID16: bf16 operands, float16 out0 / aux (row stride % 8)")
+    else:
+        name = _sym16(name, A, out0, out1, aux)
+    call(name, st, epi, M, N, K, ptr(A), A.stride(0), ptr(B), B.stride(0),
          ptr(bias), float(alpha), ptr(out0), out0.stride(0), ptr(out1),
          out1.stride(0) if out1 is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
          ptr(ws), ws.numel() if ws is not None else 0)

@@ -549,9 +549,11 @@ def encode_image(img, p, cfg: ClipConfig, method="vanilla", peft_encoder="none",
     x = torch.cat([cls, x], dim=1)                                              # :759-763
     x = x + p["visual.positional_embedding"]                                    # :764
     variant = tower_variant(method, peft_encoder, "image")
-    # the MI355X fused adapter tower's half residual stream (round_bf16.resid above)
-    xr = (getattr(rt, "resid", identity)
-          if variant == "adapter" and cfg.vision_width in (512, 768) else identity)
+    # the MI355X image tower's half residual stream (round_bf16.resid above): the adapter tower
+    # (its gradient in half too, in the backward-faithful rounding), the LoRA tower (forward)
+    xr = identity
+    if cfg.vision_width in (512, 768) and hasattr(rt, "resid"):
+        xr = rt.resid if variant == "adapter" else round_f16 if variant == "lora" else identity
     x = xr(layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"]))  # :766
     vis, _ = tower_prefixes(cfg)
     for i, pre in enumerate(vis):

@@ -912,3 +912,28 @@ def test_adapter_wgrad_unscaled(ops, dev):
         outs.append(bufs)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 8, 11])
+def test_gemm_resid16(ops, dev, tile):
+    """EPI_RESID16 (out0 half = aux_half + A B^T + bias: the LoRA / vanilla towers' residual add
+    in the half residual stream) on every tile kernel: bit-exact on small integers (every value
+    below 2^11, so exact in half), ragged M."""
+    from lcclip import _lib
+    lib = _lib.load()
+    M, N, K = 4096 + 197, 768, 128
+    g = torch.Generator(device=dev).manual_seed(tile + 40)
+    A = torch.randint(-3, 4, (M, K), device=dev, generator=g).to(BF)
+    B = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(BF)
+    bias = torch.randint(-8, 9, (N,), device=dev, generator=g).float()
+    aux = torch.randint(-500, 500, (M, N), device=dev, generator=g).to(H16)
+    out = torch.full((M, N), float("nan"), device=dev, dtype=H16)
+    try:
+        assert lib.lc_gemm_set_tile(tile) == 0
+        ops.gemm_nt(A, B, ops.EPI_RESID16, out, bias=bias, aux=aux)
+    finally:
+        lib.lc_gemm_set_tile(0)
+    ref = A.float() @ B.float().t() + bias + aux.float()
+    assert torch.equal(out, ref.to(H16))
+    with pytest.raises(TypeError):
+        ops.gemm_nt(A, B, ops.EPI_RESID16, out.float(), bias=bias, aux=aux)
