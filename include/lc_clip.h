@@ -209,6 +209,18 @@ int lc_adapter_ln_fwd_x16(hipStream_t stream, int M, int D, const void* z, long 
                           const unsigned long long* seed_dev, const void* resid, void* xout,
                           long ldx, void* hout, const float* gamma, const float* beta, void* y,
                           long ldy, float* mean, float* rstd);
+/* lc_layernorm_fwd_fp8 / lc_layernorm_bwd_fp8 over a half x: the prompt towers (MVP, MaPLe),
+ * whose prompt rows the reference casts to the stream's dtype (mvp_clip.py:256-257,
+ * maple.py:243), with their QKV / c_fc / c_proj GEMMs on the fp8 MFMA. */
+int lc_layernorm_fwd_fp8_x16(hipStream_t stream, int rows, int D, const void* x, long ldx,
+                             const int* row_idx, const float* gamma, const float* beta, void* y,
+                             long ldy, float* mean, float* rstd, void* q, long ldq, void* q_scale,
+                             long q_rows);
+int lc_layernorm_bwd_fp8_x16(hipStream_t stream, int rows, int D, const void* dy, int dy_f32,
+                             long ldy, const void* x, long ldx, const float* mean,
+                             const float* rstd, const float* gamma, const float* dres, float* dx,
+                             void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
+                             void* q_scale, long q_rows);
 
 /* im2col of NCHW f32 images into bf16 patches [n*g*g, 3*P*P] in conv1's (c, kh, kw) order.
  * Replaces: the input side of conv1 (model.py:756-758). */
@@ -334,6 +346,13 @@ int lc_lora_grad(hipStream_t stream, int M, int N, int K, int r, const void* dY,
 int lc_lora_grad_ws(hipStream_t stream, int M, int N, int K, int r, const void* dY, long ldy,
                     const void* X, long ldx, const void* apad, long lda, const void* btpad,
                     long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes);
+/* lc_lora_grad_ws whose sums are divided by *gscale (device f32: the power-of-two scale the
+ * image tower's half residual gradient carries, lc_layernorm_bwd_g16; exact) before the
+ * scaling and the accumulation. bf16 storage build only. */
+int lc_lora_grad_ws_unscaled(hipStream_t stream, int M, int N, int K, int r, const void* dY,
+                             long ldy, const void* X, long ldx, const void* apad, long lda,
+                             const void* btpad, long ldbt, float scaling, float* dA, float* dB,
+                             void* ws, long ws_bytes, const float* gscale);
 
 /* xout = resid + z + scale*(drop(relu(z Wd^T + bd)) Wu^T + bu); h (bf16 [M,64]) is saved.
  * keep = 1 - dropout p; the counter-based dropout mask is selected by

@@ -489,6 +489,31 @@ int lc_layernorm_bwd_g16(hipStream_t st, int rows, int D, const void* dy, int dy
   return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
                 row_idx, nullptr, 0, nullptr, 0, 1, 1);
 }
+
+// the prompt towers' (MVP, MaPLe) half residual stream under fp8 GEMMs: x IEEE half
+int lc_layernorm_fwd_fp8_x16(hipStream_t st, int rows, int D, const void* x, long ldx,
+                             const int* row_idx, const float* gamma, const float* beta, void* y,
+                             long ldy, float* mean, float* rstd, void* q, long ldq, void* q_scale,
+                             long q_rows) {
+  LC_CHECK_ARG(D % 256 == 0 && q != nullptr && q_scale != nullptr && ldq >= D && ldq % 16 == 0 &&
+               ((uintptr_t)q & 15) == 0 && q_rows >= (rows + 255) / 256 * 256 && q_rows % 256 == 0);
+  LC_CHECK_ARG(x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0);
+  return ln_fwd(st, rows, D, x, ldx, row_idx, gamma, beta, y, 0, ldy, mean, rstd, q, ldq, q_scale,
+                q_rows, 1);
+}
+
+int lc_layernorm_bwd_fp8_x16(hipStream_t st, int rows, int D, const void* dy, int dy_f32,
+                             long ldy, const void* x, long ldx, const float* mean,
+                             const float* rstd, const float* gamma, const float* dres, float* dx,
+                             void* dx_bf16, long ldo, const int* row_idx, void* q, long ldq,
+                             void* q_scale, long q_rows) {
+  LC_CHECK_ARG(D % 256 == 0 && q != nullptr && q_scale != nullptr && ldq >= D && ldq % 16 == 0 &&
+               ((uintptr_t)q & 15) == 0 && q_rows % 256 == 0 && row_idx == nullptr &&
+               q_rows >= (rows + 255) / 256 * 256);
+  LC_CHECK_ARG(x != nullptr && ldx % 4 == 0 && ((uintptr_t)x & 7) == 0);
+  return ln_bwd(st, rows, D, dy, dy_f32, ldy, x, ldx, mean, rstd, gamma, dres, dx, dx_bf16, ldo,
+                row_idx, q, ldq, q_scale, q_rows, 1);
+}
 #endif
 
 int lc_layernorm_bwd_fp8(hipStream_t st, int rows, int D, const void* dy, int dy_f32, long ldy,

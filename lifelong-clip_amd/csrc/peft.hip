@@ -839,7 +839,8 @@ lora_grad1p_kernel(int M, const bf16_t* __restrict__ X, long ldx, const bf16_t* 
 // order (deterministic); 32 outputs per 256-thread workgroup.
 __global__ void __launch_bounds__(256)
 lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats, long nb,
-                   float s, float* __restrict__ dA, float* __restrict__ dB) {
+                   float s, float* __restrict__ dA, float* __restrict__ dB,
+                   const float* __restrict__ div) {
   __shared__ float red[8][33];
   const int lo = threadIdx.x & 31, wg = threadIdx.x >> 5;
   const long e = (long)blockIdx.x * 32 + lo;
@@ -860,6 +861,7 @@ lora_reduce_kernel(const float* __restrict__ part, int walkers, long slot_floats
     float tot = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) tot += red[k][lo];
+    if (div) tot /= *div;  // the scaled half gradient's power of two: exact
     if (e < nb) dB[e] += s * tot;
     else dA[e - nb] += s * tot;
   }
@@ -1330,9 +1332,10 @@ int lc_lora_grad(hipStream_t st, int M, int N, int K, int r, const void* dY, lon
   LC_LAUNCH_RET();
 }
 
-int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
-                    const void* X, long ldx, const void* apad, long lda, const void* btpad,
-                    long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes) {
+static int lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
+                        const void* X, long ldx, const void* apad, long lda, const void* btpad,
+                        long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes,
+                        const float* div) {
   LC_CHECK_ARG(M > 0 && r >= 1 && r <= 4 && dY && X && apad && btpad && dA && dB && ws);
   LC_CHECK_ARG(ldy % 8 == 0 && ldx % 8 == 0 && lda % 8 == 0 && ldbt % 8 == 0);
   LC_CHECK_ARG(ldy >= N && ldx >= K && lda >= K && ldbt >= N);
@@ -1360,9 +1363,27 @@ int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, 
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return LC_ELAUNCH;
   hipLaunchKernelGGL(lora_reduce_kernel, dim3((unsigned)((slot + 31) / 32)), dim3(256), 0, st,
-                     part, walkers, slot, (long)N * r, scaling, dA, dB);
+                     part, walkers, slot, (long)N * r, scaling, dA, dB, div);
   LC_LAUNCH_RET();
 }
+
+int lc_lora_grad_ws(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
+                    const void* X, long ldx, const void* apad, long lda, const void* btpad,
+                    long ldbt, float scaling, float* dA, float* dB, void* ws, long ws_bytes) {
+  return lora_grad_ws(st, M, N, K, r, dY, ldy, X, ldx, apad, lda, btpad, ldbt, scaling, dA, dB, ws,
+                      ws_bytes, nullptr);
+}
+
+#ifndef LC_F16  // the image tower's half residual gradient (bf16 storage build only)
+int lc_lora_grad_ws_unscaled(hipStream_t st, int M, int N, int K, int r, const void* dY, long ldy,
+                             const void* X, long ldx, const void* apad, long lda,
+                             const void* btpad, long ldbt, float scaling, float* dA, float* dB,
+                             void* ws, long ws_bytes, const float* gscale) {
+  LC_CHECK_ARG(gscale != nullptr);
+  return lora_grad_ws(st, M, N, K, r, dY, ldy, X, ldx, apad, lda, btpad, ldbt, scaling, dA, dB, ws,
+                      ws_bytes, gscale);
+}
+#endif
 
 // The adapter as two skinny GEMMs through lc_gemm_nt's LDS-staged MFMA template (the weights
 // are staged once per workgroup by global_load_lds instead of being re-read by every wave):

@@ -89,9 +89,11 @@ F16_ENTRY_POINTS = ("lc_gemm_nt", "lc_gemm_nt_ws", "lc_gemm_tn", "lc_gemm_tn_ws"
 SIGNATURES.update({n + "_f16": SIGNATURES[n] for n in F16_ENTRY_POINTS})
 # the image tower's half residual stream (include/lc_clip.h "x16"): the f32 forms' arguments
 SIGNATURES.update({n + "_x16": SIGNATURES[n] for n in (
-    "lc_layernorm_fwd", "lc_layernorm_bwd", "lc_vit_embed_ln", "lc_adapter_ln_fwd")})
+    "lc_layernorm_fwd", "lc_layernorm_bwd", "lc_vit_embed_ln", "lc_adapter_ln_fwd",
+    "lc_layernorm_fwd_fp8", "lc_layernorm_bwd_fp8")})
 SIGNATURES["lc_layernorm_bwd_g16"] = SIGNATURES["lc_layernorm_bwd"]
 SIGNATURES["lc_adapter_wgrad_ws_unscaled"] = SIGNATURES["lc_adapter_wgrad_ws"] + [P]
+SIGNATURES["lc_lora_grad_ws_unscaled"] = SIGNATURES["lc_lora_grad_ws"] + [P]
 
 _lib = None
 

@@ -250,8 +250,8 @@ class BlockStack:
     def forward(self, x, n_seq: int, L: int, save: bool, training: bool = False, prompts=None,
                 stop=None, replace=None, first_ln1=None, last_ln=None):
         """x: f32 [n_seq*L, D] residual stream, or float16 (the reference's autocast residual
-        dtype, model.py:194-200 / 439-442: the fused adapter tower only, with last_ln). Returns
-        (x_out, saved-per-layer or None).
+        dtype, model.py:194-200 / 439-442: the fused adapter tower with last_ln, the LoRA tower,
+        the frozen prompt towers of MVP / MaPLe). Returns (x_out, saved-per-layer or None).
 
         prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
         before that layer and dropped after it (prompt tuning, models/mvp_clip.py:158-175: cat
@@ -281,12 +281,12 @@ class BlockStack:
         # (ops.adapter_ln_fwd: ln_2 of the block, ln_1 of the next one); ln1_ready carries the
         # statistics of an ln_1 the previous block already wrote into tmp_h
         fuse_ln = (self.variant == "adapter" and q_h is None and D in (512, 768) and self.FUSE_LN)
-        if xdt != F32 and not (q_g is None and q_h is None and not prompts and not replace
-                               and stop is None and (
-                                   (fuse_ln and last_ln is not None) or self.variant == "lora")):
+        if xdt != F32 and not (self.variant == "vanilla" or (
+                q_g is None and q_h is None and not prompts and not replace and stop is None
+                and ((fuse_ln and last_ln is not None) or self.variant == "lora"))):
             raise ValueError("a half residual stream runs the fused adapter tower (with its "
                              "closing LayerNorm fused: last_ln) or the LoRA tower, bf16, without "
-                             "prompt rows")
+                             "prompt rows, or the frozen (prompt) tower")
         e_resid = EPI_RESID16 if xdt == F16 else EPI_RESID
         ln1_ready = None
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
@@ -301,7 +301,7 @@ class BlockStack:
             Lx = L + P
             Mx = n_seq * Lx
             if P:
-                xe = _empty((Mx, D), F32, dev)
+                xe = _empty((Mx, D), xdt, dev)  # prompt rows cast to the stream's dtype
                 v = xe.view(n_seq, Lx, D)
                 v[:, :L] = x.view(n_seq, L, D)
                 v[:, L:] = prompts[idx]
@@ -639,6 +639,21 @@ class BlockStack:
     # LCCLIP_LORA_1P=0: the four-GEMM form (A/B experiments)
     LORA_1P = os.environ.get("LCCLIP_LORA_1P", "1") != "0"
 
+    def _lora_1p(self, r, K, N):
+        return self.LORA_1P and r <= 4 and (K, N) in ((768, 2304), (768, 768), (512, 1536),
+                                                      (512, 512))
+
+    def lora_half_grad_ok(self):
+        """Every LoRA gradient of this (LoRA) stack runs ops.lora_grad_1p, the form that divides
+        out the half residual gradient's scale."""
+        for blk in self.blocks:
+            a = blk.attn
+            for A, B in ((a.in_proj_weight_lora_A, a.in_proj_weight_lora_B),
+                         (a.out_proj.lora_A, a.out_proj.lora_B)):
+                if not self._lora_1p(A.shape[0], A.shape[1], B.shape[0]):
+                    return False
+        return True
+
     def _lora_grad(self, dY, X, A, B, scaling, grads, padded):
         """Rank-r LoRA gradients (lora.py:838-839, 1073-1074 autograd): one pass over X and dY
         (ops.lora_grad_1p: XA = X A^T and dYB = dY B per 32-row block, dB += s dY^T XA and
@@ -649,11 +664,14 @@ class BlockStack:
         M = dY.shape[0]
         r, K = A.shape
         N = B.shape[0]
-        if self.LORA_1P and r <= 4 and (K, N) in ((768, 2304), (768, 768), (512, 1536), (512, 512)):
+        gsc = getattr(self, "_gscale", None)  # dY carries the half residual gradient's scale
+        if self._lora_1p(r, K, N):
             with self._side():
                 ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, self._grad(grads, A),
-                                 self._grad(grads, B))
+                                 self._grad(grads, B), gscale=gsc)
             return
+        if gsc is not None:
+            raise ValueError("a scaled LoRA gradient runs the one-pass kernel only")
         with self._side():
             xa = _empty((M, 64), self.dt, dY.device)
             dyb = _empty((M, 64), self.dt, dY.device)
@@ -726,13 +744,17 @@ class ImageTower:
             self._key = key
 
     def embed(self, img, extra=None, keep=None):
-        """conv1 + CLS/pos + ln_pre (model.py:756-766): (x0 f32 [n*L, D], n, L).
+        """conv1 + CLS/pos + ln_pre (model.py:756-766): (x0 f32 [n*L, D], n, L); x0 float16
+        for the half residual stream (_resid16).
         extra: optional f32 [P, D] rows appended to every sequence after the positional
         embedding and before ln_pre (MaPLe's shared visual context,
         models/maple_clip/model.py:566-575); L then counts them. keep: dict that receives what
         embed_backward() needs."""
         pe, n, npch = self._patch_embed(img)
-        return self._embed_tail(pe, n, npch, extra, keep)
+        x0, n, L = self._embed_tail(pe, n, npch, extra, keep)
+        if self.stack.variant == "vanilla" and self._resid16():  # the frozen prompt towers
+            x0 = x0.half()
+        return x0, n, L
 
     def _patch_embed(self, img):
         """conv1 as a GEMM on im2col rows: (f32 [n*np, D], n, np)."""
@@ -829,11 +851,19 @@ class ImageTower:
     # forward and the x read of every LayerNorm backward. False: the f32 stream (A/Bs)
     RESID16 = True
     GRAD_EXP = 12  # the half residual gradient's scale target, 2^GRAD_EXP <= max|dL/df| s < 2^13
+    # LCCLIP_HALF_GRAD=0: a half residual stream with an f32 gradient (A/B experiments)
+    HALF_GRAD = os.environ.get("LCCLIP_HALF_GRAD", "1") != "0"
 
     def _resid16(self):
         st = self.stack
-        return (self.RESID16 and self.FUSE_EMBED and st.precision == "bf16"
-                and self.visual.width in (512, 768)
+        if not (self.RESID16 and self.visual.width in (512, 768)):
+            return False
+        if st.variant == "vanilla":
+            # the frozen prompt towers (MVP, MaPLe; bf16 or fp8 GEMMs): the reference casts
+            # their prompt rows to the stream's dtype (mvp_clip.py:256-257, maple.py:243);
+            # the residual gradient stays f32 (the prompt gradients are read from its rows)
+            return True
+        return (self.FUSE_EMBED and st.precision == "bf16"
                 and ((st.variant == "adapter" and st.FUSE_LN) or st.variant == "lora"))
 
     def embed_ln1(self, img, half=False):
@@ -885,9 +915,11 @@ class ImageTower:
         dev = df.device
         n, L = ctx["n"], ctx["L"]
         D = v.width
-        # the adapter tower's half residual stream: its gradient in half as well (the LoRA
-        # tower keeps an f32 gradient: its rank-r weight gradients take no scale)
-        half = ctx["x"].dtype == F16 and self.stack.variant == "adapter"
+        # the adapter and LoRA towers' half residual stream: its gradient in half as well (the
+        # frozen prompt towers keep an f32 gradient: their prompt gradients are its rows)
+        var = self.stack.variant
+        half = ctx["x"].dtype == F16 and self.HALF_GRAD and (
+            var == "adapter" or (var == "lora" and self.stack.lora_half_grad_ok()))
         gsc = None
         if half:
             # a per-call power-of-two gradient scale (the reference's GradScaler,

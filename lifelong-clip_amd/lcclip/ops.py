@@ -151,6 +151,9 @@ def gemm_nt_fp8(A, B, epi, out0, bias=None, alpha=1.0, out1=None, aux=None, q_ou
         raise ValueError(f"gemm_nt_fp8: epilogue {epi} needs q_out Fp8Mat [{M}, {N}]")
     if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
         raise ValueError("gemm_nt_fp8 bias must be a contiguous f32 vector of length N")
+    if epi == EPI_RESID16 and (out0.dtype != F16 or aux is None or aux.dtype != F16
+                               or out0.stride(0) % 8 or aux.stride(0) % 8):
+        raise TypeError("gemm_nt_fp8 EPI_RESID16: float16 out0 / aux (row stride % 8)")
     if q8:
         out1 = q_out.data
     st = stream_of(A.data)
@@ -212,13 +215,15 @@ def layernorm_fwd(x, weight, bias, y, mean=None, rstd=None, row_idx=None):
 
 
 def layernorm_fwd_fp8(x, weight, bias, q, mean=None, rstd=None, y=None):
-    """LayerNorm of x [rows, D] f32 straight into q, an Fp8Mat [rows, D] (the next fp8 GEMM's
-    A operand; the codes of bf16 output + quant_fp8); y: optional bf16 copy."""
-    _rowmajor(x, F32, "x")
+    """LayerNorm of x [rows, D] f32 (or float16: the half residual stream) straight into q, an
+    Fp8Mat [rows, D] (the next fp8 GEMM's A operand; the codes of bf16 output + quant_fp8);
+    y: optional bf16 copy."""
+    if x.dtype != F16:
+        _rowmajor(x, F32, "x")
     rows, D = x.shape
     if q.rows != rows or q.K != D or (y is not None and (y.dtype != BF16 or y.shape != x.shape)):
         raise ValueError("layernorm_fwd_fp8: output shape mismatch")
-    call("lc_layernorm_fwd_fp8", stream_of(x), rows, D, ptr(x), x.stride(0), None, ptr(weight),
+    call(_x16("lc_layernorm_fwd_fp8", x, y), stream_of(x), rows, D, ptr(x), x.stride(0), None, ptr(weight),
          ptr(bias), ptr(y), y.stride(0) if y is not None else 0, ptr(mean), ptr(rstd), ptr(q.data),
          q.data.stride(0), ptr(q.scales), q.rows_pad)
     return q
@@ -246,12 +251,15 @@ def layernorm_bwd(dy, x, mean, rstd, weight, dx, dx_bf16=None, dres=None, row_id
 
 def layernorm_bwd_fp8(dy, x, mean, rstd, weight, dx, dx_bf16, q, dres=None):
     """layernorm_bwd whose result is also written into q, an Fp8Mat [rows, D]: the fp8 A operand
-    of the next GEMM (the codes of dx_bf16 + quant_fp8)."""
+    of the next GEMM (the codes of dx_bf16 + quant_fp8). x f32 or float16 (the half residual
+    stream; dx and dres stay f32)."""
     rows = dy.shape[0]
     D = x.shape[1]
     if q.rows != rows or q.K != D:
         raise ValueError("layernorm_bwd_fp8: output shape mismatch")
-    call("lc_layernorm_bwd_fp8", stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
+    if dx.dtype != F32 or (dres is not None and dres.dtype != F32):
+        raise TypeError("layernorm_bwd_fp8: dx and dres are f32")
+    call(_x16("lc_layernorm_bwd_fp8", x, dy, dx_bf16), stream_of(x), rows, D, ptr(dy), 1 if dy.dtype == F32 else 0,
          dy.stride(0), ptr(x), x.stride(0), ptr(mean), ptr(rstd), ptr(weight), ptr(dres), ptr(dx),
          ptr(dx_bf16), dx.stride(0), None, ptr(q.data), q.data.stride(0), ptr(q.scales), q.rows_pad)
     return q
@@ -422,9 +430,11 @@ def lora_grad(dY, X, A, B, scaling, dA, dB):
          X.stride(0), ptr(A), ptr(B), float(scaling), ptr(dA), ptr(dB))
 
 
-def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
+def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB, gscale=None):
     """dB [N,r] += s dY^T (X A^T), dA [r,K] += s (dY B)^T X in one pass over X and dY
-    (lc_lora_grad_ws); a_pad [>=16, K] / bt_pad [>=16, N] bf16 with rows >= r zero."""
+    (lc_lora_grad_ws); a_pad [>=16, K] / bt_pad [>=16, N] bf16 with rows >= r zero. gscale:
+    device f32 [1], the power-of-two scale dY carries (the half residual gradient), divided out
+    (lc_lora_grad_ws_unscaled)."""
     _rowmajor(dY, HALF, "dY")
     _rowmajor(X, HALF, "X")
     _rowmajor(a_pad, HALF, "a_pad")
@@ -441,9 +451,16 @@ def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB):
         if t.dtype != F32 or not t.is_contiguous() or not t.is_cuda:
             raise ValueError(f"lora_grad_1p: {name} must be a contiguous f32 device tensor")
     ws = splitk_workspace(torch.cuda.current_stream(dY.device))
-    call(_sym16("lc_lora_grad_ws", dY, X, a_pad, bt_pad), stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
+    name = _sym16("lc_lora_grad_ws", dY, X, a_pad, bt_pad)
+    extra = ()
+    if gscale is not None:
+        if name != "lc_lora_grad_ws" or gscale.dtype != F32 or gscale.numel() != 1 \
+                or not gscale.is_cuda:
+            raise TypeError("lora_grad_1p: gscale is a device f32 [1] of the bf16 build")
+        name, extra = "lc_lora_grad_ws_unscaled", (ptr(gscale),)
+    call(name, stream_of(dY), M, N, K, r, ptr(dY), dY.stride(0), ptr(X), X.stride(0),
          ptr(a_pad), a_pad.stride(0), ptr(bt_pad), bt_pad.stride(0), float(scaling), ptr(dA),
-         ptr(dB), ptr(ws), ws.numel())
+         ptr(dB), ptr(ws), ws.numel(), *extra)
 
 
 def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=None):

@@ -431,7 +431,18 @@ def fp8_rounding(base=None):
     def rt(x):
         return base(x)
     rt.fp8 = True
+    if hasattr(base, "resid"):
+        rt.resid = base.resid
     return rt
+
+
+def prompt_tower_resid(cfg: ClipConfig, rt):
+    """The frozen prompt towers' residual rounding (MVP, MaPLe): IEEE half on the MI355X image
+    tower at widths 512 / 768 (lcclip ImageTower._resid16), forward only (straight-through: the
+    residual gradient stays f32 there); identity for the fp32 oracle. The reference casts the
+    prompt rows to the stream's dtype (mvp_clip.py:256-257, maple.py:243), so they are rounded
+    with the stream."""
+    return round_f16 if cfg.vision_width in (512, 768) and hasattr(rt, "resid") else identity
 
 
 def merged_lora_weight(w, a, bmat, scaling, rt=identity):
@@ -549,11 +560,12 @@ def encode_image(img, p, cfg: ClipConfig, method="vanilla", peft_encoder="none",
     x = torch.cat([cls, x], dim=1)                                              # :759-763
     x = x + p["visual.positional_embedding"]                                    # :764
     variant = tower_variant(method, peft_encoder, "image")
-    # the MI355X image tower's half residual stream (round_bf16.resid above): the adapter tower
-    # (its gradient in half too, in the backward-faithful rounding), the LoRA tower (forward)
+    # the MI355X image tower's half residual stream (round_bf16.resid above): the adapter and
+    # LoRA towers (their gradient in half too, in the backward-faithful rounding), the frozen
+    # tower (forward)
     xr = identity
     if cfg.vision_width in (512, 768) and hasattr(rt, "resid"):
-        xr = rt.resid if variant == "adapter" else round_f16 if variant == "lora" else identity
+        xr = rt.resid if variant in ("adapter", "lora") else round_f16
     x = xr(layer_norm(x, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"]))  # :766
     vis, _ = tower_prefixes(cfg)
     for i, pre in enumerate(vis):
@@ -967,13 +979,14 @@ def mvp_forward(img, tokens, p, cfg: ClipConfig, mvp: dict, pos_g=(0, 1), len_g=
     [pool, E, W]}. Returns (logits [B, C] (masked when use_mask), similarity_loss, image
     features [B, E], text features [C, E], mask [B, C], topk [B, 1])."""
     vis, _ = tower_prefixes(cfg)
-    x0 = mvp_embed(img, p, cfg, rt)
+    xr = prompt_tower_resid(cfg, rt)
+    x0 = xr(mvp_embed(img, p, cfg, rt))
     B, N, W = x0.shape
     with torch.no_grad():                                                       # :196-218
         q = x0.clone()
         stop = len(vis) if use_last_layer else len(vis) - 1
         for pre in vis[:stop]:
-            q = block(q, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
+            q = block(q, p, pre, cfg.vision_heads, False, "vanilla", rt=rt, xr=xr)
         query = layer_norm(q[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"])
     distance = 1 - F.cosine_similarity(query.unsqueeze(1), mvp["key"], dim=-1)  # :224-225
     topk = distance.topk(1, dim=1, largest=False)[1]                            # :231-232
@@ -986,8 +999,8 @@ def mvp_forward(img, tokens, p, cfg: ClipConfig, mvp: dict, pos_g=(0, 1), len_g=
     x = x0
     for i, pre in enumerate(vis):                                               # :163-175
         if i in prompts:
-            x = torch.cat([x, prompts[i]], dim=1)
-        x = block(x, p, pre, cfg.vision_heads, False, "vanilla", rt=rt)
+            x = torch.cat([x, xr(prompts[i])], dim=1)
+        x = block(x, p, pre, cfg.vision_heads, False, "vanilla", rt=rt, xr=xr)
         x = x[:, :N]
     x = rt(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
     img_f = linear(x, p["visual.proj"].t(), None, rt)                          # :259-261
@@ -1058,12 +1071,14 @@ def maple_forward(img, tokens, p, cfg: ClipConfig, mp: dict, n_ctx=3, depth=3, r
     cls = p["visual.class_embedding"].reshape(1, 1, W).expand(N, 1, W)
     xi = torch.cat([cls, xi], dim=1) + p["visual.positional_embedding"]
     xi = torch.cat([xi, shared.unsqueeze(0).expand(N, -1, -1)], dim=1)        # :568-570
-    xi = layer_norm(xi, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"])    # :575
+    xr = prompt_tower_resid(cfg, rt_img)
+    xi = xr(layer_norm(xi, p["visual.ln_pre.weight"], p["visual.ln_pre.bias"]))  # :575
     vis, _ = tower_prefixes(cfg)
     for i, pre in enumerate(vis):
         if 1 <= i <= len(deep_vis):
-            xi = torch.cat([xi[:, :-n_ctx], deep_vis[i - 1].unsqueeze(0).expand(N, -1, -1)], dim=1)
-        xi = block(xi, p, pre, cfg.vision_heads, False, "vanilla", rt=rt_img)
+            xi = torch.cat([xi[:, :-n_ctx], xr(deep_vis[i - 1]).unsqueeze(0).expand(N, -1, -1)],
+                           dim=1)
+        xi = block(xi, p, pre, cfg.vision_heads, False, "vanilla", rt=rt_img, xr=xr)
     xi = rt_img(layer_norm(xi[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
     img_f = linear(xi, p["visual.proj"].t(), None, rt_img)
     logits, _, _ = clip_logits(img_f, txt_f, p["logit_scale"])                # :244-250

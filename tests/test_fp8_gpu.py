@@ -124,6 +124,26 @@ def test_gemm_fp8_epilogues(ops, dev):
     assert rel(om, 0.5 * ref * aux.float()) < 4e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(4096 + 197, 768, 256), (12608, 768, 3072)])
+def test_gemm_fp8_resid16(ops, dev, M, N, K):
+    """EPI_RESID16 on the fp8 GEMM (MaPLe's c_proj forward in the half residual stream): out0
+    half = aux_half + A B^T + bias, bit-exact on small integers (|v| <= 3: exact e4m3 codes under
+    any block scale, every sum below 2^11), ragged M and a split-K launch (K = 3072)."""
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    A = torch.randint(-3, 4, (M, K), device=dev, generator=g).float()
+    B = torch.randint(-1, 2, (N, K), device=dev, generator=g).float()
+    bias = torch.randint(-8, 9, (N,), device=dev, generator=g).float()
+    aux = torch.randint(-500, 500, (M, N), device=dev, generator=g).to(torch.float16)
+    out = torch.full((M, N), float("nan"), device=dev, dtype=torch.float16)
+    ops.gemm_nt_fp8(ops.quant_fp8(A), ops.quant_fp8(B), ops.EPI_RESID16, out, bias=bias, aux=aux)
+    ref = A @ B.t() + bias + aux.float()
+    assert ref.abs().max() < 2048
+    assert torch.equal(out, ref.to(torch.float16))
+    with pytest.raises(TypeError):
+        ops.gemm_nt_fp8(ops.quant_fp8(A), ops.quant_fp8(B), ops.EPI_RESID16, out.float(),
+                        bias=bias, aux=aux)
+
+
 @pytest.mark.parametrize("M,N,K", [(4096 + 131, 3072, 768), (1000, 768, 3072), (12608, 3072, 768)])
 def test_gemm_fp8_q8_epilogues_match_quant(ops, dev, M, N, K):
     """The fp8-output epilogues (GELU_D_Q8 / MUL_Q8: MaPLe's c_fc forward and c_proj dX) give
@@ -158,13 +178,16 @@ def test_gemm_fp8_q8_epilogues_match_quant(ops, dev, M, N, K):
     same(q, ops.quant_fp8(om))
 
 
+@pytest.mark.parametrize("xdt", [torch.float32, torch.float16], ids=["x32", "x16"])
 @pytest.mark.parametrize("rows,D", [(12608, 768), (300, 1024), (77, 256)])
-def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D):
+def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D, xdt):
     """LayerNorm straight into the fp8 operand format (MaPLe's ln_1 / ln_2 in fp8 mode) equals
-    the bf16 LayerNorm followed by quant_fp8 bit for bit, with the same saved statistics."""
+    the bf16 LayerNorm followed by quant_fp8 bit for bit, with the same saved statistics; x f32
+    or IEEE half (the half residual stream: lc_layernorm_fwd_fp8_x16)."""
     g = torch.Generator(device=dev).manual_seed(rows + D)
     x = torch.randn(rows, D, device=dev, generator=g) * 3 + 1
     x[5] = 0  # a constant row: all-zero normalised blocks when beta is 0 there
+    x = x.to(xdt)
     w = torch.randn(D, device=dev, generator=g)
     b = torch.randn(D, device=dev, generator=g)
     b[:32] = 0
@@ -180,14 +203,16 @@ def test_layernorm_fwd_fp8_matches_quant(ops, dev, rows, D):
     assert torch.equal(y2, y) and torch.equal(m2, m1) and torch.equal(r2, r1)
 
 
+@pytest.mark.parametrize("xdt", [torch.float32, torch.float16], ids=["x32", "x16"])
 @pytest.mark.parametrize("rows,D", [(50432 // 16, 768), (301, 256), (1, 512)])
-def test_layernorm_bwd_fp8_matches_quant(ops, dev, rows, D):
+def test_layernorm_bwd_fp8_matches_quant(ops, dev, rows, D, xdt):
     """LayerNorm backward writing its result also as the fp8 operand of the next c_proj dX GEMM
     (the fp8 towers' block output gradient) equals the bf16 LayerNorm backward followed by
     quant_fp8 bit for bit, with identical f32 / bf16 outputs; with and without the residual
-    gradient, and a zero output-gradient row (all-zero blocks)."""
+    gradient, and a zero output-gradient row (all-zero blocks); x f32 or IEEE half
+    (lc_layernorm_bwd_fp8_x16)."""
     g = torch.Generator(device=dev).manual_seed(rows * 7 + D)
-    x = torch.randn(rows, D, device=dev, generator=g) * 2 + 0.5
+    x = (torch.randn(rows, D, device=dev, generator=g) * 2 + 0.5).to(xdt)
     w = torch.randn(D, device=dev, generator=g)
     b = torch.randn(D, device=dev, generator=g)
     y = torch.empty(rows, D, device=dev, dtype=BF)

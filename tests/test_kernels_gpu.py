@@ -914,6 +914,34 @@ def test_adapter_wgrad_unscaled(ops, dev):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("K,N", [(768, 2304), (768, 768)])
+def test_lora_grad_unscaled(ops, dev, K, N):
+    """lc_lora_grad_ws_unscaled (the LoRA tower's half residual gradient) divides the summed
+    gradients by the device scale before the scaling and the +=: a power of two, so exactly the
+    unscaled launch's result on unscaled operands (config 4's 25 216 rows, r = 4)."""
+    torch.manual_seed(K + N)
+    M, r, s = 25216, 4, 2.0 ** 12
+    dY = (torch.randn(M, N, device=dev) * 1e-3).to(BF)
+    X = torch.randn(M, K, device=dev).to(BF)
+    a_pad = torch.zeros(16, K, device=dev, dtype=BF)
+    bt_pad = torch.zeros(16, N, device=dev, dtype=BF)
+    a_pad[:r] = torch.randn(r, K, device=dev).to(BF)
+    bt_pad[:r] = torch.randn(r, N, device=dev).to(BF)
+    dA0, dB0 = torch.randn(r, K, device=dev), torch.randn(N, r, device=dev)
+    outs = []
+    for scaled in (False, True):
+        dA, dB = dA0.clone(), dB0.clone()
+        if scaled:
+            ops.lora_grad_1p((dY.float() * s).to(BF), X, a_pad, bt_pad, r, 0.25, dA, dB,
+                             gscale=torch.full((1,), s, device=dev))
+        else:
+            ops.lora_grad_1p(dY, X, a_pad, bt_pad, r, 0.25, dA, dB)
+        outs.append((dA, dB))
+    assert not torch.equal(outs[0][0], dA0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 8, 11])
 def test_gemm_resid16(ops, dev, tile):
     """EPI_RESID16 (out0 half = aux_half + A B^T + bias: the LoRA / vanilla towers' residual add

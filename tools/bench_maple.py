@@ -28,6 +28,8 @@ def main():
 
 def run(prec):
     from lcclip.maple import MaPLe
+    from lcclip.engine import ImageTower
+    ImageTower.RESID16 = os.environ.get("RESID32", "0") == "0"  # A/B: f32 residual stream
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = MaPLe("ViT-B/16", n_ctx=3, device=dev, precision=prec)
@@ -65,7 +67,8 @@ def run(prec):
                       "images_per_s": round(B / dt, 1),
                       "dtype": "fp8 e4m3 (image QKV/c_fc/c_proj fwd+dX), bf16 elsewhere"
                       if prec == "fp8" else "bf16",
-                      "data": "synthetic"}), flush=True)
+                      "data": "synthetic",
+                      "image_residual_dtype": "f16" if ImageTower.RESID16 else "f32"}), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,8 @@ WARM = int(os.environ.get("WARM", 3))
 
 def main():
     from lcclip.mvp_clip import CLIP_MVP
+    from lcclip.engine import ImageTower
+    ImageTower.RESID16 = os.environ.get("RESID32", "0") == "0"  # A/B: f32 residual stream
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = CLIP_MVP(model_name="ViT-B/16", device=dev, num_classes=C, use_last_layer=False)
@@ -66,7 +68,8 @@ def main():
     print(json.dumps({"workload": "mvp_clip ViT-B/16 prompt tuning (config 3 per-GPU shape)",
                       "per_gpu_batch": B, "classes": C, "ms_per_step": round(dt * 1e3, 3),
                       "images_per_s": round(B / dt, 1), "query_pass_ms": round(q_ms, 3),
-                      "dtype": "bf16", "data": "synthetic"}), flush=True)
+                      "dtype": "bf16", "data": "synthetic",
+                      "image_residual_dtype": "f16" if ImageTower.RESID16 else "f32"}), flush=True)
 
 
 if __name__ == "__main__":
