@@ -770,12 +770,14 @@ def test_vit_embed_ln_matches_separate(ops, dev, n, npch, D):
 H16 = torch.float16
 
 
-@pytest.mark.parametrize("M,D,keep", [(4096 + 7, 768, 0.9), (1000, 512, 1.0), (50432, 768, 0.9)])
+@pytest.mark.parametrize("M,D,keep", [(4096 + 7, 768, 0.9), (1000, 512, 1.0), (50432, 768, 0.9),
+                                      (16 * 256 * 3 + 5, 512, 0.9)])
 def test_adapter_ln_fwd_x16(ops, dev, M, D, keep):
     """lc_adapter_ln_fwd_x16 (resid and x_out in IEEE half, the reference's autocast residual
     dtype) against the f32 kernel on the same half inputs: x_out is the f32 result rounded to
     half, bit for bit (the same arithmetic, then one RNE rounding); h bit-identical; the
-    LayerNorm reads x_out as stored (statistics and y against torch fp32 on the half values)."""
+    LayerNorm reads x_out as stored (statistics and y against torch fp32 on the half values).
+    The cases run walkers over 1, 2, 4 and 13 blocks, ragged last blocks included."""
     torch.manual_seed(M + D)
     z = torch.randn(M, D, device=dev).to(BF)
     Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
