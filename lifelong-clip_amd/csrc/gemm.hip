@@ -2124,9 +2124,14 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     const int t256 = ((M + 255) / 256) * (N / 256), cus = cu_count();
     const int full = t256 / cus, rem = t256 % cus;
     const bool tail_ok = full >= 2 || rem == 0 || 2 * rem >= cus || (2 * rem <= cus && K >= 1024);
+    // N = 768 with one full round and a short ragged tail that split-K cannot spread (K < 1024:
+    // LoRA / MVP at 128 images, M = 25 216 .. 27 776, the out-projections): 128x128 at two
+    // workgroups per CU (M = 25 216, K = 768: 35.5 / 36.9 us dX / fwd vs 39.4 / 39.9 for 128x64
+    // and 42.8 / 43.7 for gemm8, tools/bench_gemm.py, profiles/r05/lo/)
     if (N % 128 != 0) tile = 4;
     else if (M >= 4096 && N % 256 == 0 && t256 >= cus && tail_ok) tile = 8;
     else if (M >= 4096 && N % 256 == 0 && 2 * t256 >= cus && K >= 2048) tile = 8;
+    else if (M >= 4096 && N <= 768 && t256 >= cus) tile = 1;
     else if (M >= 4096 && N <= 768) tile = 4;
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): gemm8 since its epilogue stores went branch-free
