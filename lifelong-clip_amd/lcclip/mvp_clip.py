@@ -17,6 +17,7 @@ reference.
 """
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Union
 
 import torch
@@ -27,6 +28,35 @@ from . import autograd as lc_autograd
 from . import clip_loader
 from .adapter_clip import EOT_TOKEN, SOT_TOKEN
 from .textcache import TokenFeatureCache
+
+
+class _PoolGather(torch.autograd.Function):
+    """table[idx] for a small pool (the selected e-prompts / masks, mvp_clip.py:236-237): the same
+    gather forward; the backward sums each selected row's gradient into its pool entry as one
+    GEMM (one_hot(idx)^T @ grad) instead of torch's sort-based index_put accumulate, which
+    serialises the 128 images that pick the same few entries (0.39 ms per config-3 step)."""
+
+    @staticmethod
+    def forward(ctx, table, idx):
+        ctx.save_for_backward(idx)
+        ctx.pool = table.shape[0]
+        return table[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        flat = idx.reshape(-1)
+        onehot = F.one_hot(flat, ctx.pool).to(g.dtype)
+        gt = onehot.t() @ g.reshape(flat.numel(), -1)
+        return gt.reshape(ctx.pool, *g.shape[idx.dim():]), None
+
+
+# LCCLIP_POOL_GEMM=0: plain indexing (torch's index_put backward), for A/Bs
+_POOL_GEMM = os.environ.get("LCCLIP_POOL_GEMM", "1") != "0"
+
+
+def _pool_gather(table, idx):
+    return _PoolGather.apply(table, idx) if _POOL_GEMM else table[idx]
 
 
 class CLIP_MVP(nn.Module):
@@ -193,8 +223,8 @@ class CLIP_MVP(nn.Module):
         topk = scaled_distance.topk(self.selection_size, dim=1, largest=False)[1]
         distance = distance[torch.arange(topk.size(0), device=topk.device).unsqueeze(1).repeat(
             1, self.selection_size), topk].squeeze().clone()
-        e_prompts = self.e_prompts[topk].squeeze().clone()
-        mask = self.mask[topk].mean(1).squeeze().clone()
+        e_prompts = _pool_gather(self.e_prompts, topk).squeeze().clone()
+        mask = _pool_gather(self.mask, topk).mean(1).squeeze().clone()
         if self.use_contrastiv:
             key_wise_distance = 1 - F.cosine_similarity(self.key.unsqueeze(1), self.key, dim=-1)
             self.similarity_loss = -((key_wise_distance[topk] / mass[topk]).exp().mean() /
