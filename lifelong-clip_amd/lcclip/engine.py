@@ -255,7 +255,9 @@ class BlockStack:
 
         prompts: optional {layer: f32 [n_seq, P, D]} — prompt tokens appended to every sequence
         before that layer and dropped after it (prompt tuning, models/mvp_clip.py:158-175: cat
-        along the sequence, block, x[:N]); that layer runs at L + P. stop: run layers [0, stop)
+        along the sequence, block, x[:N]); that layer runs at L + P. Consecutive prompt layers
+        with one prompt count keep the rows between them and overwrite them (the same values
+        without the compact / expand copies). stop: run layers [0, stop)
         only (the MVP query pass, models/mvp_clip.py:211-216). replace: optional
         {layer: (row, f32 [P, D] or [n_seq, P, D])} — rows [row, row + P) of every sequence are
         overwritten before that layer (MaPLe's deep compound prompts,
@@ -289,6 +291,8 @@ class BlockStack:
                              "prompt rows, or the frozen (prompt) tower")
         e_resid = EPI_RESID16 if xdt == F16 else EPI_RESID
         ln1_ready = None
+        n_run = len(self.blocks) if stop is None else min(stop, len(self.blocks))
+        carried = 0  # prompt rows x carries from the previous layer (kept: same count here)
         for idx, (blk, st) in enumerate(zip(self.blocks, self.staged)):
             if stop is not None and idx >= stop:
                 break
@@ -300,7 +304,13 @@ class BlockStack:
             P = P_of.get(idx, 0)
             Lx = L + P
             Mx = n_seq * Lx
-            if P:
+            inherit = bool(P) and carried == P
+            if inherit:
+                # the previous layer's prompt rows are dropped and this layer's appended in their
+                # place (models/mvp_clip.py:163-175: x[:N] then cat): overwrite them in x, which
+                # no saved tensor aliases (the previous layer saved its input, not its output)
+                x.view(n_seq, Lx, D)[:, L:] = prompts[idx]
+            elif P:
                 xe = _empty((Mx, D), xdt, dev)  # prompt rows cast to the stream's dtype
                 v = xe.view(n_seq, Lx, D)
                 v[:, :L] = x.view(n_seq, L, D)
@@ -407,15 +417,22 @@ class BlockStack:
                 s.update(z2=z2, hd2=hd2)
             else:
                 wpr(e_resid, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
+            # a run of prompt layers with one prompt count keeps the rows between them (no
+            # compact-and-expand copies): the next layer overwrites them
+            keep = (self.PROMPT_KEEP and bool(P) and idx + 1 < n_run
+                    and P_of.get(idx + 1, 0) == P and not (replace and idx + 1 in replace))
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
-                         mean2=mean2, rstd2=rstd2, gd=pre, P=P)
+                         mean2=mean2, rstd2=rstd2, gd=pre, P=P, keep=keep, inherit=inherit)
                 if replace and idx in replace:
                     s["R"] = (replace[idx][0], replace[idx][1].shape[-2])
                 if self.variant == "lora":
                     s["h1"] = h1
                 saved.append(s)
-            x = x_out if not P else x_out.view(n_seq, Lx, D)[:, :L].reshape(n_seq * L, D)
+            if not P or keep:
+                x, carried = x_out, (P if keep else 0)
+            else:
+                x, carried = x_out.view(n_seq, Lx, D)[:, :L].reshape(n_seq * L, D), 0
         return x, saved
 
     # ------------------------------------------------------------------ backward
@@ -491,9 +508,9 @@ class BlockStack:
             P = s.get("P", 0)
             Lx = L + P
             Mx = n_seq * Lx
-            if P:
-                if len(pairs) == 2:
-                    pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
+            if P and len(pairs) == 2:
+                pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
+            if P and not s.get("keep"):  # (kept rows: the gradient is already in the Lx layout)
                 e = 2 if cur != 2 else 1
                 q_of.clear()
                 for src, dst in zip(pairs[cur], pairs[e]):
@@ -576,9 +593,16 @@ class BlockStack:
                 v = ox.view(n_seq, Lx, D)
                 if prompt_grads is not None:
                     prompt_grads[li] = v[:, L:].clone()
-                # compact into the (consumed) expanded pair
-                pairs[cur][0][:M].view(n_seq, L, D).copy_(v[:, :L])
-                pairs[cur][1][:M].view(n_seq, L, D).copy_(oxb.view(n_seq, Lx, D)[:, :L])
+                if s.get("inherit"):
+                    # these prompt rows replaced the previous layer's (dropped) ones: no gradient
+                    # flows into them; the layout stays Lx for the previous layer
+                    v[:, L:] = 0
+                    oxb.view(n_seq, Lx, D)[:, L:] = 0
+                    cur = out
+                else:
+                    # compact into the (consumed) expanded pair
+                    pairs[cur][0][:M].view(n_seq, L, D).copy_(v[:, :L])
+                    pairs[cur][1][:M].view(n_seq, L, D).copy_(oxb.view(n_seq, Lx, D)[:, :L])
             else:
                 cur = out
         self.sync_grads()
@@ -634,6 +658,9 @@ class BlockStack:
                               gscale=getattr(self, "_gscale", None))
         return dz
 
+    # LCCLIP_PROMPT_KEEP=0: compact and re-expand between prompt layers of one prompt count
+    # (A/B experiments)
+    PROMPT_KEEP = os.environ.get("LCCLIP_PROMPT_KEEP", "1") != "0"
     # LCCLIP_MERGE_BATCH=0: one lc_merge_weight launch per LoRA merge / cast (A/B experiments)
     MERGE_BATCH = os.environ.get("LCCLIP_MERGE_BATCH", "1") != "0"
     # LCCLIP_LORA_1P=0: the four-GEMM form (A/B experiments)
