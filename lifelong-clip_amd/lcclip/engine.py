@@ -419,18 +419,18 @@ class BlockStack:
                 wpr(e_resid, x_out, bias=blk.mlp.c_proj.bias, aux=x_mid)
             # a run of prompt layers with one prompt count keeps the rows between them (no
             # compact-and-expand copies): the next layer overwrites them
-            keep = (self.PROMPT_KEEP and bool(P) and idx + 1 < n_run
-                    and P_of.get(idx + 1, 0) == P and not (replace and idx + 1 in replace))
+            pkeep = (self.PROMPT_KEEP and bool(P) and idx + 1 < n_run
+                     and P_of.get(idx + 1, 0) == P and not (replace and idx + 1 in replace))
             if save:
                 s.update(x_in=x, mean1=mean1, rstd1=rstd1, qkv=qkv, O=O, lse=lse, x_mid=x_mid,
-                         mean2=mean2, rstd2=rstd2, gd=pre, P=P, keep=keep, inherit=inherit)
+                         mean2=mean2, rstd2=rstd2, gd=pre, P=P, pkeep=pkeep, inherit=inherit)
                 if replace and idx in replace:
                     s["R"] = (replace[idx][0], replace[idx][1].shape[-2])
                 if self.variant == "lora":
                     s["h1"] = h1
                 saved.append(s)
-            if not P or keep:
-                x, carried = x_out, (P if keep else 0)
+            if not P or pkeep:
+                x, carried = x_out, (P if pkeep else 0)
             else:
                 x, carried = x_out.view(n_seq, Lx, D)[:, :L].reshape(n_seq * L, D), 0
         return x, saved
@@ -510,7 +510,7 @@ class BlockStack:
             Mx = n_seq * Lx
             if P and len(pairs) == 2:
                 pairs.append((_empty((Mmax, D), F32, dev), _empty((Mmax, D), self.dt, dev)))
-            if P and not s.get("keep"):  # (kept rows: the gradient is already in the Lx layout)
+            if P and not s.get("pkeep"):  # (kept rows: the gradient is already in the Lx layout)
                 e = 2 if cur != 2 else 1
                 q_of.clear()
                 for src, dst in zip(pairs[cur], pairs[e]):
