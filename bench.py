@@ -457,6 +457,12 @@ def main():
             "text_tower_dtype": {"fp16": "f16", "bf16": "bf16"}[args.text_precision],
             # the image tower's residual stream (the reference's autocast dtype: fp16)
             "image_residual_dtype": "f16" if trainer.img._resid16() else "f32",
+            # and its gradient (fp16 under a per-call power-of-two scale: the GradScaler's role)
+            "image_residual_grad_dtype": "f16" if (
+                trainer.img._resid16() and trainer.img.HALF_GRAD and (
+                    trainer.img.stack.variant == "adapter" or (
+                        trainer.img.stack.variant == "lora"
+                        and trainer.img.stack.lora_half_grad_ok()))) else "f32",
             "data": "synthetic (random-init ViT-B/16 CLIP weights, U[0,1) images normalised with "
                     "CIFAR-100 stats, random prompt token ids)",
             "config": {"workload": f"{args.method}_clip ViT-B/16 both towers, online_train step "
