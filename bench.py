@@ -73,10 +73,15 @@ def synthetic_batch(B, C, dev, seed, tok_seed=7):
     return x, tok.to(dev), y.to(dev)
 
 
-def routes_to_pp(M, N, K, epi):
+def routes_to_pp(M, N, K, epi, cus=256):
     """The lc_gemm_nt tile selector's rule for the 256x256 phase-interleaved kernel (gemm.hip,
     lc_gemm_nt_ex -> gemm8_kernel): the dominant kernel of the step."""
-    return N % 128 == 0 and M >= 4096 and N % 256 == 0 and (M + 255) // 256 * (N // 256) >= 256
+    if N % 256 or M < 4096 or K <= 64:
+        return False
+    t256 = (M + 255) // 256 * (N // 256)
+    full, rem = divmod(t256, cus)
+    tail_ok = full >= 2 or rem == 0 or 2 * rem >= cus or (2 * rem <= cus and K >= 1024)
+    return (t256 >= cus and tail_ok) or (2 * t256 >= cus and K >= 2048)
 
 
 class GemmTimer:
