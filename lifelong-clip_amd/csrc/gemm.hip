@@ -2133,6 +2133,10 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     else if (M >= 4096 && N % 256 == 0 && 2 * t256 >= cus && K >= 2048) tile = 8;
     else if (M >= 4096 && N <= 768 && t256 >= cus) tile = 1;
     else if (M >= 4096 && N <= 768) tile = 4;
+    // few rows, narrow N, long K (the C = 10 text tower's c_proj fwd / c_fc dX / QKV dX at
+    // M = 770): 128x64 tiles give twice the workgroups of 128x128 for the long reduction
+    // (15.6 / 15.5 / 12.6 vs 22.4 / 22.3 / 17.8 us, profiles/r05/tw/)
+    else if (N <= 768 && K >= 1536) tile = 4;
     else tile = 1;
     // c_proj dX x QuickGELU' (N 3072, K 768): gemm8 since its epilogue stores went branch-free
     // (260 vs 267-271 us for the 4-wave kernel standalone, step +0.4 %, profiles/r03/s2/

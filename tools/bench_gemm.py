@@ -19,11 +19,12 @@ if os.environ.get("LCLIB"):  # an experimental build of the library
 from lcclip._lib import call, ptr, stream_of  # noqa: E402
 
 M = int(os.environ.get("M", 50432))
+W = int(os.environ.get("W", 768))  # the tower width (512: the text tower's shapes)
 SHAPES = [  # (name, M, N, K, epi)
-    ("qkv_fwd", M, 2304, 768, ops.EPI_BF16), ("out_fwd", M, 768, 768, ops.EPI_BF16),
-    ("fc1_fwd", M, 3072, 768, ops.EPI_GELU_D), ("fc2_fwd", M, 768, 3072, ops.EPI_BF16),
-    ("fc2_dx", M, 3072, 768, ops.EPI_MUL), ("fc1_dx", M, 768, 3072, ops.EPI_BF16),
-    ("out_dx", M, 768, 768, ops.EPI_BF16), ("qkv_dx", M, 768, 2304, ops.EPI_BF16),
+    ("qkv_fwd", M, 3 * W, W, ops.EPI_BF16), ("out_fwd", M, W, W, ops.EPI_BF16),
+    ("fc1_fwd", M, 4 * W, W, ops.EPI_GELU_D), ("fc2_fwd", M, W, 4 * W, ops.EPI_BF16),
+    ("fc2_dx", M, 4 * W, W, ops.EPI_MUL), ("fc1_dx", M, W, 4 * W, ops.EPI_BF16),
+    ("out_dx", M, W, W, ops.EPI_BF16), ("qkv_dx", M, W, 3 * W, ops.EPI_BF16),
 ]
 if os.environ.get("SQUARE"):
     SHAPES += [("sq4096", 4096, 4096, 4096, ops.EPI_BF16), ("sq8192", 8192, 8192, 8192, ops.EPI_BF16)]
