@@ -96,6 +96,32 @@ def test_mvp_tiny_forward_and_grads(dev, use_last_layer):
     assert m.features.shape == (B, cfg.vision_width)
 
 
+def test_mvp_prompt_rows_kept_is_exact(dev, monkeypatch):
+    """Keeping the prompt rows between consecutive prompt layers of one prompt count (layers 0-1:
+    5 g-prompt rows, 2-4: 20 e-prompt rows; BlockStack.PROMPT_KEEP) only removes the compact /
+    expand copies: logits and all four gradients are bit-identical to the copying form."""
+    from lcclip.engine import BlockStack
+    cfg = o.TINY_MVP
+    sd = o.synthetic_state_dict(cfg, seed=22)
+    mv = o.mvp_params(cfg, seed=6)
+    img = o.synthetic_images(3, cfg.image_resolution, seed=7).to(dev)
+    tok = o.synthetic_tokens(4, cfg.context_length, seed=7, vocab=cfg.vocab_size).to(dev)
+    y = torch.tensor([0, 3, 1], device=dev)
+    out = []
+    for keep in (True, False):
+        monkeypatch.setattr(BlockStack, "PROMPT_KEEP", keep)
+        m = build(cfg, sd, mv, dev, use_last_layer=False)
+        m.train()
+        m.text_tokens = tok
+        logits = m(img, tok)
+        m.loss_fn(logits, y).backward()
+        torch.cuda.synchronize()
+        out.append((logits.detach(), *[getattr(m, k).grad.clone()
+                                       for k in ("key", "mask", "g_prompts", "e_prompts")]))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_mvp_vit_b16_shapes(dev):
     """Full ViT-B/16: 197 tokens, 202 at layers 0-1 and 217 at layers 2-4 (config 3's shapes),
     B = 2, C = 4; forward vs the oracle in both rounding modes, prompt gradients vs fp32."""
