@@ -189,3 +189,21 @@ def test_rowgrad_buffer_reuse_zeroes_stale_rows():
     assert d.shape[0] == 30
     use(2, 7, idx=torch.tensor([3, 9], dtype=torch.int32), key=None)   # EOT-style rows
     use(2, 7, idx=torch.tensor([4, 12], dtype=torch.int32), key=None)
+
+
+@pytest.mark.parametrize("shape,idx_shape", [((10, 60, 8), (128, 1)), ((10, 200), (7, 2)),
+                                             ((5, 3, 4), (3,))])
+def test_mvp_pool_gather_matches_indexing(shape, idx_shape):
+    """MVP's pool gather (lcclip.mvp_clip._PoolGather: the selected e-prompts / masks with a
+    one_hot^T @ grad backward) equals table[idx] and its index_put backward (float64, exact)."""
+    from lcclip.mvp_clip import _PoolGather
+    torch.manual_seed(sum(shape))
+    t = torch.randn(*shape, dtype=torch.float64, requires_grad=True)
+    idx = torch.randint(0, shape[0], idx_shape)
+    a = _PoolGather.apply(t, idx)
+    g = torch.randn_like(a)
+    (ga,) = torch.autograd.grad(a, t, g)
+    b = t[idx]
+    (gb,) = torch.autograd.grad(b, t, g)
+    assert torch.equal(a, b)
+    assert torch.allclose(ga, gb, rtol=0, atol=1e-12)
