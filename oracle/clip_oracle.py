@@ -90,11 +90,13 @@ def round_f16(x):
     return x + (r - x).detach()
 
 
-# The MI355X image tower keeps the fused adapter tower's residual stream in IEEE half, the
-# reference's autocast dtype (model.py:194-200: its LayerNorm returns the input dtype, so x is
-# fp16 from conv1 through every `x = x + ...`; lcclip ImageTower.RESID16, widths 512 / 768):
-# encode_image rounds x there with the image rounding's ``resid`` hook (straight-through: the
-# residual gradient stays f32 on the GPU).
+# The MI355X image towers keep the residual stream in IEEE half, the reference's autocast dtype
+# (model.py:194-200: its LayerNorm returns the input dtype, so x is fp16 from conv1 through every
+# `x = x + ...`; lcclip ImageTower.RESID16, widths 512 / 768): encode_image / mvp_forward /
+# maple_forward round x there with the image rounding's ``resid`` hook. round_f16 is
+# straight-through; the backward-faithful ``Rounding.resid`` also rounds the residual gradient
+# under the per-call scale (the adapter and LoRA towers' half gradient; the frozen prompt towers
+# keep an f32 gradient on the GPU).
 round_bf16.resid = round_f16
 
 
@@ -517,8 +519,9 @@ def block(x, p, pre, n_head, causal, variant, lora_scaling=0.25, rt=identity, ma
     (model.py:439-442; one adapter module reused for both sub-blocks, Q6). x is the residual
     stream [N, L, D]; xr rounds it after each residual add (the half residual stream)."""
     # gq: the backward's bf16 gradient stores (rt.bwd; identity for the fp32 oracle and the
-    # straight-through round_bf16): the residual stream's gradient stays f32 and each sub-block
-    # reads its bf16 copy (dx_midb / the layer's output pair, engine.py BlockStack.backward);
+    # straight-through round_bf16): each sub-block reads the bf16 copy of the residual stream's
+    # gradient (dx_midb / the layer's output pair, engine.py BlockStack.backward; the gradient
+    # itself is f32 or, through xr, half);
     # dz, dO, da (c_proj dX x QuickGELU'), dh (c_fc dX, QKV dX) are bf16
     gq = getattr(rt, "bwd", identity)
     gelu = getattr(rt, "gelu", quick_gelu)
