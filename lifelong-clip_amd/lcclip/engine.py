@@ -873,9 +873,10 @@ class ImageTower:
     # (False: the three separate launches, for A/Bs)
     FUSE_EMBED = True
     # the residual stream in IEEE half, the reference's autocast dtype (model.py:194-200: its
-    # LayerNorm returns the input dtype, so x is fp16 from conv1 through every block; here the
-    # fused adapter tower: lc_*_x16): a third less HBM traffic in the fused adapter + LayerNorm
-    # forward and the x read of every LayerNorm backward. False: the f32 stream (A/Bs)
+    # LayerNorm returns the input dtype, so x is fp16 from conv1 through every block; the fused
+    # adapter, LoRA and frozen prompt towers: lc_*_x16, LC_EPI_RESID16): a third less HBM traffic
+    # in the residual adds, the fused adapter + LayerNorm forward and the x read of every
+    # LayerNorm backward. False: the f32 stream (A/Bs)
     RESID16 = True
     GRAD_EXP = 12  # the half residual gradient's scale target, 2^GRAD_EXP <= max|dL/df| s < 2^13
     # LCCLIP_HALF_GRAD=0: a half residual stream with an f32 gradient (A/B experiments)
