@@ -850,11 +850,22 @@ class ImageTower:
         ops.layernorm_fwd(x, v.ln_post.weight, v.ln_post.bias, lnp, mean, rstd, row_idx=cls_idx)
         return lnp, cls_idx, mean, rstd
 
-    def query(self, x0, n, L, stop=None):
+    def query(self, x0, n, L, stop=None, first_ln1=None):
         """The MVP key query (models/mvp_clip.py:196-218): blocks [0, stop) on x0 without
-        saving, then ln_post of the CLS rows (f32 [n, D], no projection)."""
-        x, _ = self.stack.forward(x0, n, L, save=False, stop=stop)
+        saving, then ln_post of the CLS rows (f32 [n, D], no projection). first_ln1: layer 0's
+        ln_1 of x0 from embed_query()."""
+        x, _ = self.stack.forward(x0, n, L, save=False, stop=stop, first_ln1=first_ln1)
         return self._ln_post(x, n, L, F32)[0]
+
+    def embed_query(self, img):
+        """embed() for the MVP passes, (x0, n, L, first_ln1 or None): the half residual stream's
+        fused embed (conv1 rows -> CLS / pos -> ln_pre -> x0 in half, and layer 0's ln_1 for the
+        key query, which runs on x0 unchanged) where it applies, else embed()."""
+        if (self.FUSE_EMBED and self._resid16() and self.stack.variant == "vanilla"
+                and self.stack.precision == "bf16"):
+            return self.embed_ln1(img, half=True)
+        x0, n, L = self.embed(img)
+        return x0, n, L, None
 
     def forward(self, img, save: bool, training: bool = False, prompts=None):
         """img -> (features f32 [n, E], ctx). prompts: {layer: f32 [n, P, D]} appended before

@@ -211,9 +211,9 @@ class CLIP_MVP(nn.Module):
         vis = self.backbone.visual
         tower = vis.tower
         with torch.no_grad():
-            x0, n, L = tower.embed(inputs)
+            x0, n, L, first = tower.embed_query(inputs)
             stop = vis.layers if self.use_last_layer else vis.layers - 1
-            query = tower.query(x0, n, L, stop)
+            query = tower.query(x0, n, L, stop, first_ln1=first)
         B = n
         if self.training:
             self.features = torch.cat((self.features, query.detach().cpu()), dim=0)

@@ -23,6 +23,7 @@ def main():
     from lcclip.mvp_clip import CLIP_MVP
     from lcclip.engine import ImageTower
     ImageTower.RESID16 = os.environ.get("RESID32", "0") == "0"  # A/B: f32 residual stream
+    ImageTower.FUSE_EMBED = os.environ.get("FUSE_EMBED", "1") != "0"  # A/B: the separate embed
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     m = CLIP_MVP(model_name="ViT-B/16", device=dev, num_classes=C, use_last_layer=False)
@@ -60,8 +61,8 @@ def main():
     with torch.no_grad():
         e0.record()
         for _ in range(STEPS):
-            x0, n, L = vis.tower.embed(x)
-            vis.tower.query(x0, n, L, vis.layers - 1)
+            x0, n, L, first = vis.tower.embed_query(x)
+            vis.tower.query(x0, n, L, vis.layers - 1, first_ln1=first)
         e1.record()
     torch.cuda.synchronize()
     q_ms = e0.elapsed_time(e1) / STEPS
