@@ -351,6 +351,10 @@ def main():
                     help="replay the step as a HIP graph (1 GPU; measured equal to eager at B=256)")
     ap.add_argument("--text-precision", default="fp16", choices=["fp16", "bf16"],
                     help="the text tower's 16-bit storage (AdapterCLIP text_precision)")
+    ap.add_argument("--image-precision", default="bf16", choices=["bf16", "fp16"],
+                    help="the image tower's 16-bit storage (AdapterCLIP image_precision): bf16 is "
+                         "BASELINE config 2's; fp16 is the reference's autocast arithmetic "
+                         "(a parity mode, reported beside the bf16 headline)")
     ap.add_argument("--gemm-tile", type=int, default=0,
                     help="A/B knob: lc_gemm_set_tile value for every GEMM (0 = automatic)")
     ap.add_argument("--streamk", type=int, default=None,
@@ -392,7 +396,7 @@ def main():
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
     model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev,
-                        text_precision=args.text_precision)
+                        text_precision=args.text_precision, image_precision=args.image_precision)
     trainer = OnlineTrainer(model, distributed=dp,
                             shard_text=os.environ.get("LCCLIP_DP_NOSHARD") != "1",
                             overlap_text=os.environ.get("LCCLIP_OVERLAP_TEXT", "1") != "0",
@@ -458,7 +462,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": {"bf16": "bf16", "fp16": "f16"}[args.image_precision],
             "text_tower_dtype": {"fp16": "f16", "bf16": "bf16"}[args.text_precision],
             # the image tower's residual stream (the reference's autocast dtype: fp16)
             "image_residual_dtype": "f16" if trainer.img._resid16() else "f32",
@@ -507,7 +511,8 @@ def main():
                                  "stream, timed with HIP events around each launch of one extra "
                                  "eager step"},
             "runtime": {"GPU_MAX_HW_QUEUES": HW_QUEUES,
-                        "side_streams": 1 if trainer._merge_side_streams() else 2},
+                        "side_streams": 1 if trainer._merge_side_streams() else 2,
+                        "side_stream_cus": trainer.side_cus},
             "train_transform": tf_stats,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,3 @@
+source gpu_step.sh
+PY="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+run t_new2 900 $PY tests/test_f16_gpu.py tests/test_dp_gpu.py

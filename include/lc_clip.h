@@ -462,6 +462,19 @@ int lc_grad_pow2_normalize(hipStream_t stream, long n, float* x, float* scale, i
 /* y[i] += x[i] / scale[0] (n elements, f32): the scaled gradients back to their true size. */
 int lc_add_unscaled(hipStream_t stream, long n, float* y, const float* x, const float* scale);
 
+/* ---- streams -------------------------------------------------------------------------------
+ * The step's side streams (text tower, PEFT weight gradients) run beside the image chain's
+ * GEMMs. The reference has no counterpart: nn.DataParallel runs one replica per GPU on torch's
+ * default stream (methods/_trainer.py:167-168). A side stream confined to a subset of the CUs
+ * keeps its workgroups off the CUs the main stream's GEMM tiles refill. */
+/* n_cu[0] = the device's compute-unit count. */
+int lc_device_cu_count(int device, int* n_cu);
+/* A HIP stream on `device` whose kernels run only on CUs first, first + stride, ...,
+ * first + (count - 1) * stride (hipExtStreamCreateWithCUMask); the caller owns it
+ * (lc_stream_destroy). */
+int lc_stream_create_cumask(int device, int first, int count, int stride, void** stream);
+int lc_stream_destroy(void* stream);
+
 /* ---- IEEE-half storage: the text tower ------------------------------------------------------
  * Each _f16 entry point is its namesake above with every 16-bit operand, output and weight
  * image in IEEE half (binary16, round-to-nearest-even) instead of bf16: same arguments, same
@@ -469,7 +482,8 @@ int lc_add_unscaled(hipStream_t stream, long n, float* y, const float* x, const 
  * The reference computes both towers under fp16 autocast (methods/adapter_clip.py:87); the
  * text tower keeps that precision here (its bf16 rounding carries half of the logits' distance
  * from fp32 and most of the C = 100 gradients'), the image tower keeps bf16
- * (BASELINE config 2). Built from the same kernel sources with -DLC_F16. */
+ * (BASELINE config 2) unless AdapterCLIP(image_precision="fp16") asks for the reference's
+ * arithmetic there too. Built from the same kernel sources with -DLC_F16. */
 int lc_gemm_nt_f16(hipStream_t stream, int epi, int M, int N, int K, const void* A, long lda,
                    const void* B, long ldb, const float* bias, float alpha, void* out0, long ldo0,
                    void* out1, long ldo1, const void* aux, long ldaux);
@@ -526,6 +540,13 @@ int lc_adapter_wgrad_f16(hipStream_t stream, int M, int D, const void* gout, lon
 int lc_adapter_wgrad_ws_f16(hipStream_t stream, int M, int D, const void* gout, long ldg,
                             const void* h, const void* z, long ldz, const void* dpre, float scale,
                             float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes);
+/* The image tower at the reference's own arithmetic (AdapterCLIP(image_precision="fp16"):
+ * conv1's im2col rows and the first ln_1 output in IEEE half, the residual stream f32). */
+int lc_patchify_f16(hipStream_t stream, int n_img, int res, int patch, const float* img, void* out);
+int lc_vit_embed_ln_f16(hipStream_t stream, int n_img, int n_patch, int D, const float* patch,
+                        const float* cls, const float* pos, const float* ln_pre_w,
+                        const float* ln_pre_b, float* x0, const float* ln1_w, const float* ln1_b,
+                        void* y, float* mean1, float* rstd1);
 
 #ifdef __cplusplus
 }

@@ -295,4 +295,39 @@ int lc_add_unscaled(hipStream_t st, long n, float* y, const float* x, const floa
   LC_LAUNCH_RET();
 }
 
+int lc_device_cu_count(int device, int* n_cu) {
+  LC_CHECK_ARG(n_cu != nullptr);
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return LC_ELAUNCH;
+  *n_cu = v;
+  return LC_OK;
+}
+
+int lc_stream_create_cumask(int device, int first, int count, int stride, void** stream) {
+  int n_cu = 0;
+  LC_CHECK_ARG(stream != nullptr && first >= 0 && count > 0 && stride > 0);
+  if (lc_device_cu_count(device, &n_cu) != LC_OK) return LC_ELAUNCH;
+  LC_CHECK_ARG((long)first + (long)(count - 1) * stride < n_cu);
+  uint32_t mask[32] = {0};
+  LC_CHECK_ARG(n_cu <= 32 * 32);
+  for (int i = 0; i < count; ++i) {
+    const int cu = first + i * stride;
+    mask[cu >> 5] |= 1u << (cu & 31);
+  }
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return LC_ELAUNCH;
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)((n_cu + 31) / 32), mask);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return LC_ELAUNCH;
+  *stream = (void*)s;
+  return LC_OK;
+}
+
+int lc_stream_destroy(void* stream) {
+  LC_CHECK_ARG(stream != nullptr);
+  return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? LC_OK : LC_ELAUNCH;
+}
+
 }  // extern "C"

@@ -77,6 +77,9 @@ SIGNATURES = {
     "lc_head_feat_grad": [P, c_int, c_int, c_int, P, c_long, c_long, P, P, P, P, P, P],
     "lc_grad_pow2_normalize": [P, c_long, P, P, c_int],
     "lc_add_unscaled": [P, c_long, P, P, P],
+    "lc_device_cu_count": [c_int, P],
+    "lc_stream_create_cumask": [c_int, c_int, c_int, c_int, P],
+    "lc_stream_destroy": [P],
 }
 
 # the IEEE-half (text tower) forms: same arguments (include/lc_clip.h, "IEEE-half storage")
@@ -85,7 +88,7 @@ F16_ENTRY_POINTS = ("lc_gemm_nt", "lc_gemm_nt_ws", "lc_gemm_tn", "lc_gemm_tn_ws"
                     "lc_cast_bf16", "lc_merge_weight", "lc_cast_weights_bf16",
                     "lc_merge_weights_bf16", "lc_lora_grad", "lc_lora_grad_ws", "lc_adapter_fwd",
                     "lc_adapter_ln_fwd", "lc_adapter_bwd", "lc_adapter_wgrad",
-                    "lc_adapter_wgrad_ws")
+                    "lc_adapter_wgrad_ws", "lc_patchify", "lc_vit_embed_ln")
 SIGNATURES.update({n + "_f16": SIGNATURES[n] for n in F16_ENTRY_POINTS})
 # the image tower's half residual stream (include/lc_clip.h "x16"): the f32 forms' arguments
 SIGNATURES.update({n + "_x16": SIGNATURES[n] for n in (

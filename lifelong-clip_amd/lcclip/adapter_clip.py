@@ -26,7 +26,8 @@ EOT_TOKEN = 49407
 
 class AdapterCLIP(nn.Module):
     def __init__(self, model_name, peft_method="adapter", peft_encoder="both", device=None,
-                 tokenizer=None, arch_overrides=None, text_precision="fp16"):
+                 tokenizer=None, arch_overrides=None, text_precision="fp16",
+                 image_precision="bf16"):
         super().__init__()
         self.device = device
         design_details = {
@@ -44,6 +45,21 @@ class AdapterCLIP(nn.Module):
         self.prompt_template = "a bad photo of a {}."
         self._tokenizer = tokenizer
         self.set_text_precision(text_precision)
+        self.set_image_precision(image_precision)
+
+    def set_image_precision(self, precision):
+        """The image tower's 16-bit storage: 'bf16' (default; BASELINE config 2 names bf16 for
+        the throughput configuration: half residual stream, bf16 GEMM / attention operands) or
+        'fp16' (the reference's own arithmetic, torch.cuda.amp.autocast fp16 at
+        methods/adapter_clip.py:87: IEEE-half GEMM / attention operands, an f32 residual stream,
+        and the backward on a per-call power-of-two gradient scale, the GradScaler's role at
+        :93). Extension of the reference surface, like set_text_precision."""
+        dt = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(precision)
+        if dt is None:
+            raise ValueError("image_precision must be 'fp16' or 'bf16'")
+        self.model.visual.tower.stack.set_storage(dt)
+        self.image_precision = precision
+        return self
 
     def set_text_precision(self, precision):
         """The text tower's 16-bit storage: 'fp16' (default; IEEE half, the precision the
@@ -59,7 +75,7 @@ class AdapterCLIP(nn.Module):
 
     @classmethod
     def from_state_dict(cls, state_dict, peft_method="adapter", peft_encoder="both", device=None,
-                        tokenizer=None, text_precision="fp16"):
+                        tokenizer=None, text_precision="fp16", image_precision="bf16"):
         """Build from an in-memory CLIP state dict (the path clip_loader.load takes for a local
         checkpoint file, clip_loader.py:116-135)."""
         from .model import build_model
@@ -76,6 +92,7 @@ class AdapterCLIP(nn.Module):
         self.dtype = self.model.dtype
         self.prompt_template = "a bad photo of a {}."
         self._tokenizer = tokenizer
+        self.set_image_precision(image_precision)
         return self.set_text_precision(text_precision)
 
     @property

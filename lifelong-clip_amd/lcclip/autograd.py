@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 
 from . import ops
+from .engine import ScaledGrads
 from .ops import F32
 
 
@@ -58,12 +59,24 @@ class _StackFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        dy = dy.contiguous().float().clone()
+        grads = {p: torch.zeros(p.shape, dtype=F32, device=p.device) for p in ctx.params}
+        sg = None
+        if ctx.stack.dt == torch.float16:
+            # IEEE-half storage: the incoming gradient (mostly below half's normal range at
+            # ViT-B/16) is scaled by a power of two first and every result divided by it again,
+            # as the fused towers do (engine.ScaledGrads; the GradScaler's role,
+            # methods/adapter_clip.py:93)
+            sg = ScaledGrads(ctx.stack, dy)
+            dy, g_run = sg.df, sg.grads
+        else:
+            dy, g_run = dy.contiguous().float().clone(), grads
         dyb = torch.empty(dy.shape, dtype=ctx.stack.dt, device=dy.device)
         ops.cast_bf16(dy, dyb)
-        grads = {p: torch.zeros(p.shape, dtype=F32, device=p.device) for p in ctx.params}
-        dx, _ = ctx.stack.backward(ctx.saved_list, dy, dyb, grads, ctx.n_seq, ctx.L)
+        dx, _ = ctx.stack.backward(ctx.saved_list, dy, dyb, g_run, ctx.n_seq, ctx.L)
         ctx.saved_list = None
+        if sg is not None:
+            sg.add_to(grads)
+            dx = sg.unscaled(dx)
         return (None, dx, None, None, None, None, *[grads[p] for p in ctx.params])
 
 

@@ -5,6 +5,12 @@ global batch (methods/adapter_clip.py:84-89, _trainer.py:168); the backbone is f
 is per-image CE over class logits, so images shard along the batch with no data-path collective.
 What remains is:
 
+  * replicas: the reference's DataParallel re-broadcasts every parameter and buffer from GPU 0
+    on every forward (replicate -> broadcast_coalesced, _trainer.py:167-168). Here the
+    weights are replicated ONCE, when the trainer is built: rank 0's frozen backbone, buffers and
+    flat PEFT parameters are broadcast to every rank (broadcast_from_root), and from then on the
+    ranks stay identical because they apply the same averaged gradients with the same AdamW.
+
   * PEFT gradients: averaged over ranks. They live in one flat fp32 buffer; per-layer-group
     buckets are all-reduced asynchronously as soon as backward has finished those layers, so
     the exchange overlaps the rest of backward (RCCL runs on its own stream; on gloo the same
@@ -40,6 +46,39 @@ class DataParallel:
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.active = self.world > 1 or (self.enabled and os.environ.get("LCCLIP_DP_FORCE") == "1")
         self._works = []
+
+    # ---------------------------------------------------------------- replication
+    def root_rank(self):
+        """The global rank of the group's rank 0."""
+        if self.group is None:
+            return 0
+        return dist.get_global_rank(self.group, 0)
+
+    def broadcast_from_root(self, tensors, bucket_bytes=64 << 20):
+        """Overwrite `tensors` (in place) with rank 0's values, once. Same-dtype tensors on one
+        device go in flattened buckets of about `bucket_bytes` (a few large broadcasts instead of
+        one per tensor: the ViT-B/16 backbone is ~300 tensors, 600 MB in f32)."""
+        if not self.active:
+            return
+        src = self.root_rank()
+        groups = {}
+        for t in tensors:
+            groups.setdefault((t.dtype, t.device), []).append(t)
+        for (dtype, device), ts in groups.items():
+            bucket, nbytes = [], 0
+            for t in ts + [None]:
+                if t is not None:
+                    bucket.append(t)
+                    nbytes += t.numel() * t.element_size()
+                if bucket and (t is None or nbytes >= bucket_bytes):
+                    flat = torch.cat([b.detach().reshape(-1) for b in bucket])
+                    dist.broadcast(flat, src=src, group=self.group)
+                    off = 0
+                    with torch.no_grad():
+                        for b in bucket:
+                            b.copy_(flat[off:off + b.numel()].view_as(b))
+                            off += b.numel()
+                    bucket, nbytes = [], 0
 
     # ---------------------------------------------------------------- prompt sharding
     def prompt_slice(self, C: int):

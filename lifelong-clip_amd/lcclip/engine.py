@@ -118,6 +118,14 @@ class BlockStack:
         for st in self.staged:
             st.peft_key = None
 
+    def invalidate_all(self):
+        """Forget every staged weight image, frozen ones included (their source tensors were
+        overwritten in place without a version bump, e.g. by a broadcast)."""
+        for st in self.staged:
+            st.frozen_key = None
+            st.peft_key = None
+            st.q_key = None
+
     def stage(self):
         casts, merges = [], []
         for blk, st in zip(self.blocks, self.staged):
@@ -712,6 +720,59 @@ class BlockStack:
             ops.gemm_tn(dyb, X, self._grad(grads, A), alpha=scaling)
 
 
+class ScaledGrads:
+    """A backward run on a power-of-two-scaled incoming gradient (IEEE-half storage: its 16-bit
+    gradient copies sit mostly below half's normal range at ViT-B/16, 1e-9..3e-4). The scale is
+    computed on the device (ops.grad_pow2_normalize: the role of the reference's GradScaler,
+    methods/adapter_clip.py:93); the stack's PEFT gradients accumulate in a zeroed scratch
+    buffer and are added to the caller's divided by that scale, and so are any f32 input /
+    prompt gradients (exact: a power of two, no host sync, no skipped steps)."""
+
+    def __init__(self, stack, df, target_exp=10):
+        dev = df.device
+        self.stack = stack
+        self.df = df.contiguous().float().clone()
+        self.scale = _empty((1,), F32, dev)
+        ops.grad_pow2_normalize(self.df, self.scale, target_exp=target_exp)
+        params = stack.trainable_params()
+        self.flat = torch.zeros(sum(p.numel() for p in params), dtype=F32, device=dev)
+        self.grads, off = {}, 0
+        for p in params:
+            self.grads[p] = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def add_to(self, dst):
+        """dst[p] += scratch[p] / scale: one launch when dst's buffers are consecutive views of
+        one flat buffer in parameter order (the trainer's flat gradient), else one per
+        parameter."""
+        params = self.stack.trainable_params()
+        if not params:
+            return
+        views = [dst[p] for p in params]
+        first = views[0]
+        contiguous = True
+        off = 0
+        for v in views:
+            if not v.is_contiguous() or v.data_ptr() != first.data_ptr() + off * 4:
+                contiguous = False
+                break
+            off += v.numel()
+        if contiguous:
+            span = torch.as_strided(first, (self.flat.numel(),), (1,))
+            ops.add_unscaled(span, self.flat, self.scale)
+            return
+        for p in params:
+            ops.add_unscaled(dst[p], self.grads[p], self.scale)
+
+    def unscaled(self, t):
+        """A fresh f32 tensor t / scale."""
+        if t is None:
+            return None
+        out = torch.zeros(t.shape, dtype=F32, device=t.device)
+        ops.add_unscaled(out.view(-1), t.contiguous().view(-1), self.scale)
+        return out
+
+
 class RowGrad:
     """The stack-output gradient pair (f32, bf16 [rows, D]) of a tower whose head reads a few
     rows per sequence: the row-gathered LayerNorm backward (ln_post at the CLS rows,
@@ -758,15 +819,16 @@ class ImageTower:
 
     def _stage(self):
         v = self.visual
-        key = _key(v.conv1.weight, v.proj)
+        dt = self.stack.dt
+        key = _key(v.conv1.weight, v.proj) + (dt,)
         if key != self._key:
             W = v.conv1.weight.shape[0]
             dev = v.conv1.weight.device
-            self.conv_w = _empty((W, v.conv1.weight[0].numel()), BF16, dev)
+            self.conv_w = _empty((W, v.conv1.weight[0].numel()), dt, dev)
             ops.merge_weight(v.conv1.weight.detach().reshape(W, -1), None, None, 0.0, self.conv_w)
             E = v.proj.shape[1]
-            self.projT = _empty((E, W), BF16, dev)      # forward: f = x @ proj  -> B = proj^T
-            self.proj = _empty((W, E), BF16, dev)       # backward: dx = df @ proj^T -> B = proj
+            self.projT = _empty((E, W), dt, dev)      # forward: f = x @ proj  -> B = proj^T
+            self.proj = _empty((W, E), dt, dev)       # backward: dx = df @ proj^T -> B = proj
             ops.merge_weight(v.proj.detach(), None, None, 0.0, self.proj, self.projT)
             self._key = key
 
@@ -797,11 +859,12 @@ class ImageTower:
             if img.dtype != BF16 or img.shape[1] != 3 * P * P or img.shape[0] % npch:
                 raise ValueError(f"patch input must be bf16 [n*{npch}, {3 * P * P}]")
             n = img.shape[0] // npch
-            patches = img.contiguous()
+            # (the fp16 tower: bf16 -> half is exact for normalised pixels, |x| < 2^15)
+            patches = img.contiguous().to(self.stack.dt)
         else:
             n = img.shape[0]
             img = img.contiguous().to(F32)
-            patches = _empty((n * npch, 3 * P * P), BF16, dev)
+            patches = _empty((n * npch, 3 * P * P), self.stack.dt, dev)
             ops.patchify(img, P, patches)
         pe = _empty((n * npch, v.width), F32, dev)
         ops.gemm_nt(patches, self.conv_w, EPI_F32, pe)
@@ -870,9 +933,6 @@ class ImageTower:
     def forward(self, img, save: bool, training: bool = False, prompts=None):
         """img -> (features f32 [n, E], ctx). prompts: {layer: f32 [n, P, D]} appended before
         that layer (prompt tuning, models/mvp_clip.py:158-175)."""
-        if self.stack.dt != BF16:
-            raise ValueError("the image tower runs on bf16 storage (BASELINE config 2); float16 "
-                             "storage is the text tower's")
         if (self.FUSE_EMBED and not prompts and self.stack.precision == "bf16"
                 and self.visual.width in (512, 768, 1024)):
             x0, n, L, first = self.embed_ln1(img, half=self._resid16())
@@ -895,7 +955,9 @@ class ImageTower:
 
     def _resid16(self):
         st = self.stack
-        if not (self.RESID16 and self.visual.width in (512, 768)):
+        if not (self.RESID16 and self.visual.width in (512, 768)) or st.dt != BF16:
+            # (the fp16 tower, image_precision="fp16": an f32 residual stream, its 16-bit
+            # operands in IEEE half)
             return False
         if st.variant == "vanilla":
             # the frozen prompt towers (MVP, MaPLe; bf16 or fp8 GEMMs): the reference casts
@@ -914,7 +976,7 @@ class ImageTower:
         L, D = npch + 1, v.width
         dev = pe.device
         x0 = _empty((n * L, D), F16 if half else F32, dev)
-        y = _empty((n * L, D), BF16, dev)
+        y = _empty((n * L, D), self.stack.dt, dev)
         mean1 = _empty((n * L,), F32, dev)
         rstd1 = _empty((n * L,), F32, dev)
         ln1 = self.stack.blocks[0].ln_1
@@ -940,7 +1002,7 @@ class ImageTower:
             ci = cls_idx.long()
             lnp, mean, rstd = last["y"][ci], last["mean"][ci], last["rstd"][ci]
         else:
-            lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, BF16)
+            lnp, cls_idx, mean, rstd = self._ln_post(x, n, L, self.stack.dt)
         f = _empty((n, self.projT.shape[0]), F32, x.device)
         ops.gemm_nt(lnp, self.projT, EPI_F32, f)
         ctx = dict(saved=saved, x=x, cls_idx=cls_idx, mean=mean, rstd=rstd, n=n, L=L,
@@ -954,12 +1016,14 @@ class ImageTower:
         dev = df.device
         n, L = ctx["n"], ctx["L"]
         D = v.width
+        dt = self.stack.dt
         # the adapter and LoRA towers' half residual stream: its gradient in half as well (the
         # frozen prompt towers keep an f32 gradient: their prompt gradients are its rows)
         var = self.stack.variant
         half = ctx["x"].dtype == F16 and self.HALF_GRAD and (
             var == "adapter" or (var == "lora" and self.stack.lora_half_grad_ok()))
-        gsc = None
+        gsc = sg = None
+        out_grads, out_pg = grads, prompt_grads
         if half:
             # a per-call power-of-two gradient scale (the reference's GradScaler,
             # methods/adapter_clip.py:93): max|dL/df| lands in [2^12, 2^13), which keeps the
@@ -970,18 +1034,35 @@ class ImageTower:
                 self._gsc = torch.ones(1, dtype=F32, device=dev)
             gsc = self._gsc
             ops.grad_pow2_normalize(df, gsc, target_exp=self.GRAD_EXP)
-        dfb = _empty(df.shape, BF16, dev)
+        elif dt == F16:
+            # the fp16 tower (f32 residual gradient, IEEE-half GEMM operands): the same scale,
+            # with every returned gradient divided by it again (ScaledGrads)
+            sg = ScaledGrads(self.stack, df, target_exp=self.GRAD_EXP)
+            df, grads = sg.df, sg.grads
+            prompt_grads = {} if prompt_grads is not None else None
+        dfb = _empty(df.shape, dt, dev)
         ops.cast_bf16(df.contiguous(), dfb)
         dln = _empty((n, D), F32, dev)
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
         dx, dxb = self._grad_in.get(n * L, D, dev, ctx["cls_idx"], key=(n, L),
-                                    gdt=F16 if half else F32)
+                                    dt=dt, gdt=F16 if half else F32)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, n, L, on_layer, grad_stream,
                                     need_dx=need_dx or 0 in ctx["prompt_layers"],
                                     prompt_grads=prompt_grads, keep_input=True, gscale=gsc)
+        if sg is not None:
+            sg.add_to(out_grads)
+            if out_pg is not None:
+                for k, t in prompt_grads.items():
+                    out_pg[k] = sg.unscaled(t)
+            gx = sg.unscaled(gx)
+        elif half and gx is not None:
+            # the half residual gradient carries the scale: the f32 input gradient without it
+            out = torch.zeros(gx.shape, dtype=F32, device=dev)
+            ops.add_unscaled(out.view(-1), gx.float().contiguous().view(-1), gsc)
+            gx = out
         return gx if need_dx else None
 
 
@@ -1034,27 +1115,20 @@ class TextTower:
     def backward(self, ctx, df, grads, on_layer=None, prompt_grads=None, need_dx=False):
         """Returns the input-embedding gradient (f32 [C*L, D]) when need_dx, else None.
 
-        IEEE-half storage (stack.set_storage(torch.float16)): the backward's gradients are
-        mostly below half's normal range (1e-9..3e-4 at ViT-B/16), so the incoming feature
-        gradient is first scaled by a power of two computed on the device
-        (ops.grad_pow2_normalize: the reference's GradScaler role, methods/adapter_clip.py:93),
-        the stack's PEFT gradients are accumulated into a zeroed scratch buffer and added to
-        `grads` divided by that scale (exact)."""
+        IEEE-half storage (stack.set_storage(torch.float16)): the backward runs on a
+        power-of-two-scaled incoming gradient and every gradient it returns (PEFT, prompt rows,
+        input embeddings) is divided by that scale again (ScaledGrads)."""
         c = self.clip
         dev = df.device
         C, L = ctx["C"], ctx["L"]
         D = c.transformer.width
         dt = self.stack.dt
-        scale = out_grads = None
+        sg = None
         df = df.contiguous()
+        out_grads = grads
         if dt == F16:
-            if need_dx or prompt_grads is not None:
-                raise NotImplementedError("float16 text-tower storage with input / prompt "
-                                          "gradients (MaPLe keeps the bf16 text tower)")
-            df = df.float().clone()
-            scale = _empty((1,), F32, dev)
-            ops.grad_pow2_normalize(df, scale)
-            out_grads, grads = grads, self._scratch_grads(dev)
+            sg = ScaledGrads(self.stack, df)
+            df, grads = sg.df, sg.grads
         dfb = _empty(df.shape, dt, dev)
         ops.cast_bf16(df, dfb)
         dln = _empty((C, D), F32, dev)
@@ -1062,41 +1136,13 @@ class TextTower:
         dx, dxb = self._grad_in.get(C * L, D, dev, ctx["eot"], dt=dt)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], c.ln_final.weight, dx, dxb,
                           row_idx=ctx["eot"])
+        pg = {} if (sg is not None and prompt_grads is not None) else prompt_grads
         gx, _ = self.stack.backward(ctx["saved"], dx, dxb, grads, C, L, on_layer,
-                                    need_dx=need_dx, prompt_grads=prompt_grads, keep_input=True)
-        if scale is not None:
-            self._add_unscaled(out_grads, grads, scale)
+                                    need_dx=need_dx, prompt_grads=pg, keep_input=True)
+        if sg is not None:
+            sg.add_to(out_grads)
+            gx = sg.unscaled(gx)
+            if prompt_grads is not None:
+                for k, v in pg.items():
+                    prompt_grads[k] = sg.unscaled(v)
         return gx
-
-    def _scratch_grads(self, dev):
-        """Zeroed f32 gradient buffers for the stack's PEFT parameters, views of one flat
-        buffer in parameter order."""
-        params = self.stack.trainable_params()
-        flat = torch.zeros(sum(p.numel() for p in params), dtype=F32, device=dev)
-        out, off = {}, 0
-        for p in params:
-            out[p] = flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self._scratch_flat = flat
-        return out
-
-    def _add_unscaled(self, dst, src, scale):
-        """dst[p] += src[p] / scale: one launch when dst's buffers are consecutive views of one
-        flat buffer in parameter order (the trainer's flat gradient), else one per parameter."""
-        params = self.stack.trainable_params()
-        views = [dst[p] for p in params]
-        first = views[0]
-        contiguous = all(v.is_contiguous() for v in views)
-        off = 0
-        for v in views:
-            if not contiguous or v.data_ptr() != first.data_ptr() + off * 4:
-                contiguous = False
-                break
-            off += v.numel()
-        if contiguous:
-            n = self._scratch_flat.numel()
-            span = torch.as_strided(first, (n,), (1,))
-            ops.add_unscaled(span, self._scratch_flat, scale)
-            return
-        for p in params:
-            ops.add_unscaled(dst[p], src[p], scale)

@@ -266,12 +266,16 @@ def layernorm_bwd_fp8(dy, x, mean, rstd, weight, dx, dx_bf16, q, dres=None):
 
 
 def patchify(img, patch, out):
+    """NCHW f32 images -> conv1's im2col rows, bf16 or float16 (out's type)."""
     if img.dtype != F32 or not img.is_contiguous():
         raise ValueError("patchify expects a contiguous f32 NCHW batch")
     n, c, h, w = img.shape
     if c != 3 or h != w:
         raise ValueError("patchify expects square 3-channel images")
-    call("lc_patchify", stream_of(img), n, h, patch, ptr(img), ptr(out))
+    g = h // patch
+    if out.dtype not in HALF or not out.is_contiguous() or out.numel() != n * g * g * 3 * patch * patch:
+        raise ValueError("patchify: out must be contiguous bf16 / float16 [n*patches, 3*p*p]")
+    call(_sym16("lc_patchify", out), stream_of(img), n, h, patch, ptr(img), ptr(out))
     return out
 
 
@@ -287,8 +291,10 @@ def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, m
     block's ln_1 -> y (bf16), mean1, rstd1, in one launch (lc_vit_embed_ln[_x16])."""
     D = x0.shape[1]
     rows = n_img * (n_patch + 1)
+    # y bf16, or float16 with an f32 x0 (the fp16 image tower: lc_vit_embed_ln_f16)
     if tuple(x0.shape) != (rows, D) or tuple(y.shape) != (rows, D) or x0.dtype not in (F32, F16) \
-            or y.dtype != BF16 or not x0.is_contiguous() or not y.is_contiguous() \
+            or y.dtype not in ((BF16, F16) if x0.dtype == F32 else (BF16,)) \
+            or not x0.is_contiguous() or not y.is_contiguous() \
             or tuple(patch_emb.shape) != (n_img * n_patch, D) or not patch_emb.is_contiguous():
         raise ValueError("vit_embed_ln: shape / layout mismatch")
     # every other operand is read raw by the kernel: f32, contiguous, of the sizes it assumes
@@ -298,7 +304,7 @@ def vit_embed_ln(patch_emb, cls, pos, ln_pre_w, ln_pre_b, ln1_w, ln1_b, x0, y, m
         if t.dtype != F32 or not t.is_contiguous() or t.numel() != numel or t.device != x0.device:
             raise ValueError(f"vit_embed_ln: {name} must be contiguous f32 with {numel} elements "
                              f"on {x0.device}")
-    call(_x16("lc_vit_embed_ln", x0), stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
+    call(_x16("lc_vit_embed_ln", x0, y), stream_of(x0), n_img, n_patch, D, ptr(patch_emb), ptr(cls), ptr(pos),
          ptr(ln_pre_w), ptr(ln_pre_b), ptr(x0), ptr(ln1_w), ptr(ln1_b), ptr(y), ptr(mean1),
          ptr(rstd1))
     return x0
@@ -464,7 +470,14 @@ def lora_grad_1p(dY, X, a_pad, bt_pad, r, scaling, dA, dB, gscale=None):
 
 
 def adapter_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, seed_dev=None):
+    """xout = resid + z + scale * up(drop(relu(down(z)))): resid / xout f32 [M, D] (the kernel
+    reads and writes them raw; a half residual stream goes through adapter_ln_fwd)."""
     M, D = z.shape
+    if resid.dtype != F32 or xout.dtype != F32:
+        raise TypeError("adapter_fwd: resid and xout must be f32")
+    if tuple(resid.shape) != (M, D) or tuple(xout.shape) != (M, D) or resid.stride() != xout.stride() \
+            or xout.stride(1) != 1:
+        raise ValueError("adapter_fwd: resid and xout must be row-major [M, D] views of one stride")
     call(_sym16("lc_adapter_fwd", z, Wd, Wu, h), stream_of(z), M, D, ptr(z), z.stride(0), ptr(Wd), ptr(bd), ptr(Wu),
          ptr(bu), float(scale), float(keep), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(seed_dev),
          ptr(resid), ptr(xout), xout.stride(0), ptr(h))
@@ -596,3 +609,37 @@ def add_unscaled(y, x, scale):
         raise ValueError("add_unscaled: contiguous f32 tensors of one size")
     call("lc_add_unscaled", stream_of(y), y.numel(), ptr(y), ptr(x), ptr(scale))
     return y
+
+
+def device_cu_count(device):
+    """Compute units of a HIP device (lc_device_cu_count)."""
+    import ctypes
+    n = ctypes.c_int(0)
+    call("lc_device_cu_count", int(torch.device(device).index or 0), ctypes.byref(n))
+    return n.value
+
+
+class CUMaskedStream:
+    """A HIP stream whose kernels run only on `count` CUs (first, first + stride, ...), wrapped
+    as a torch.cuda.ExternalStream (lc_stream_create_cumask). The HIP stream lives as long as
+    this object."""
+
+    def __init__(self, device, count, stride=1, first=0):
+        import ctypes
+        dev = torch.device(device)
+        h = ctypes.c_void_p(None)
+        call("lc_stream_create_cumask", int(dev.index or 0), int(first), int(count), int(stride),
+             ctypes.byref(h))
+        self.handle = h.value
+        self.count, self.stride, self.first = int(count), int(stride), int(first)
+        self.stream = torch.cuda.ExternalStream(self.handle, device=dev)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                torch.cuda.synchronize()
+                call("lc_stream_destroy", h)
+            except Exception:
+                pass
+            self.handle = None

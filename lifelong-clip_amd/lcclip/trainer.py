@@ -46,7 +46,7 @@ def remap_labels(labels, class_list=None):
 class OnlineTrainer:
     def __init__(self, adapter_clip, lr=5e-4, weight_decay=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  process_group=None, distributed=None, shard_text=True, bucket_layers=4,
-                 overlap_text=True, overlap_grads=True):
+                 overlap_text=True, overlap_grads=True, side_cus=None):
         self.wrapper = adapter_clip
         self.clip = adapter_clip.model
         freeze_backbone(self.wrapper)
@@ -79,6 +79,8 @@ class OnlineTrainer:
                 self.grads[p] = self.flat_g[off:off + k].view_as(p)
                 off += k
         self.params = params
+        if self.distributed:
+            self.replicate()
         self.skip = torch.zeros(1, dtype=torch.int32, device=dev)
         # AdamW's step (bias correction) lives on the device and advances only for applied
         # updates; step_count counts optimizer_step() calls, skipped ones included
@@ -89,8 +91,30 @@ class OnlineTrainer:
         self.overlap_grads = bool(overlap_grads)
         self._side = None
         self._gstream = None
+        # side streams confined to a CU subset: (count, stride, first) or None (every CU);
+        # LCCLIP_SIDE_CUS="count[,stride[,first]]" for A/Bs
+        env = os.environ.get("LCCLIP_SIDE_CUS")
+        if side_cus is None and env:
+            side_cus = tuple(int(v) for v in env.split(","))
+        self.side_cus = None if side_cus is None else (tuple(side_cus) + (1, 0)[len(side_cus) - 1:])[:3]
+        self._masked = []
         self._txt_cache = TokenFeatureCache()
         self.logit_scale = self.clip.logit_scale.detach().reshape(1)
+
+    def replicate(self):
+        """Make every rank's model rank 0's, once (the one-time form of nn.DataParallel's
+        per-step replicate, methods/_trainer.py:167-168): the frozen backbone parameters, the
+        buffers (text_tokens included) and the flat PEFT parameter buffer are broadcast from
+        rank 0, and every staged weight image is dropped so the next forward re-stages from the
+        broadcast values."""
+        peft = {id(p) for p in self.params}
+        frozen = [p for p in self.wrapper.parameters() if id(p) not in peft]
+        bufs = [b for b in self.wrapper.buffers() if b.is_floating_point() or b.dtype == torch.int64]
+        self.dp.broadcast_from_root([self.flat_p] + [p.data for p in frozen] + bufs)
+        for st in (self.img.stack, self.txt.stack):
+            st.invalidate_all()
+        self.img._key = None
+        self.txt._key = None
 
     def reset_optimizer(self):
         """online_before_task rebuilds AdamW per task (methods/adapter_clip.py:127, Q14)."""
@@ -198,21 +222,31 @@ class OnlineTrainer:
             if side is not None:
                 return side
         if self._gstream is None:
-            self._gstream = torch.cuda.Stream(device=dev)
+            self._gstream = self._new_stream(dev)
         return self._gstream
+
+    def _new_stream(self, dev):
+        if self.side_cus is None:
+            return torch.cuda.Stream(device=dev)
+        count, stride, first = self.side_cus
+        ms = ops.CUMaskedStream(dev, count, stride, first)
+        self._masked.append(ms)  # owns the HIP stream
+        return ms.stream
 
     def _merge_side_streams(self):
         """One side stream for the text tower AND the PEFT weight gradients when the process
         group is up and HIP has few hardware queues. HIP maps streams onto GPU_MAX_HW_QUEUES
-        queues (default 4); main + text + weight-gradient streams + RCCL's own is one stream too
+        queues (default 4; the value exported when lcclip was imported, which is the one HIP read if
+        it initialised after that); main + text + weight-gradient streams + RCCL's own is one stream too
         many, and the side streams then land on the main stream's queue and stop overlapping it
         (r2: 7308 vs 8172 img/s at N = 1 with the exchange forced on). Sharing one side stream
         keeps every stream on its own queue at the default. LCCLIP_SIDE_STREAMS=1|2 forces it."""
         force = os.environ.get("LCCLIP_SIDE_STREAMS")
         if force in ("1", "2"):
             return force == "1"
+        from . import HW_QUEUES_AT_IMPORT
         try:
-            queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            queues = int(HW_QUEUES_AT_IMPORT or "4")
         except ValueError:
             queues = 4
         return self.distributed and queues < 6
@@ -221,7 +255,7 @@ class OnlineTrainer:
         if not self.overlap_text:
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=dev)
+            self._side = self._new_stream(dev)
         return self._side
 
     def _img_bucket_hook(self):

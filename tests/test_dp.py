@@ -181,3 +181,40 @@ def test_single_process_is_a_noop():
     assert torch.equal(t, torch.arange(5.))
     tok = torch.arange(12).reshape(3, 4)
     assert torch.equal(dp.shard_tokens(tok), tok)
+
+
+def _replica_worker(rank, port, tmpdir, WORLD):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from lcclip import AdapterCLIP, OnlineTrainer
+    from test_surface import TINY_ARCH
+    torch.manual_seed(1234 + 17 * rank)  # a rank-dependent draw: every rank builds other weights
+    w = AdapterCLIP("tiny", peft_method="adapter", peft_encoder="both", arch_overrides=TINY_ARCH)
+    w.set_token(torch.arange(2 * 77).reshape(2, 77) % 500 + rank)  # buffers differ too
+    before = {k: v.detach().clone() for k, v in w.state_dict().items()}
+    tr = OnlineTrainer(w, distributed=True)
+    after = {k: v.detach().clone() for k, v in w.state_dict().items()}
+    torch.save({"before": before, "after": after, "flat_p": tr.flat_p.clone()},
+               os.path.join(tmpdir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("WORLD", [2, 4])
+def test_trainer_replicates_rank0_once(WORLD):
+    """verdict r5: the ranks' replicas are made identical at trainer construction (the one-time
+    form of DataParallel's per-step replicate, methods/_trainer.py:167-168), not by seeding
+    alone: ranks built from different random draws all hold rank 0's parameters and buffers
+    afterwards, PEFT views of the flat buffer included."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_replica_worker, args=(_free_port(), tmp, WORLD), nprocs=WORLD, join=True)
+        outs = [torch.load(os.path.join(tmp, f"r{r}.pt"), weights_only=True) for r in range(WORLD)]
+    r0 = outs[0]["before"]
+    for r in range(1, WORLD):
+        differ = [k for k in r0 if not torch.equal(outs[r]["before"][k], r0[k])]
+        assert differ  # the ranks did start apart
+        for k, v in r0.items():
+            assert torch.equal(outs[r]["after"][k], v), (r, k)
+        assert torch.equal(outs[r]["flat_p"], outs[0]["flat_p"])
+    for k, v in r0.items():
+        assert torch.equal(outs[0]["after"][k], v), k  # rank 0 keeps its own

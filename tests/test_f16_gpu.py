@@ -274,3 +274,38 @@ def test_text_tower_f16_vs_oracle(dev):
     assert rel(feats["fp16"], t32) < 2e-3
     assert rel(feats["bf16"], tbf) < 5e-3
     assert rel(feats["fp16"], t32) < 0.5 * rel(feats["bf16"], t32)
+
+
+def test_stack_apply_f16_scaled_backward(dev):
+    """the plain module path (Transformer.forward -> autograd stack_apply) of an
+    IEEE-half stack runs its backward on a power-of-two-scaled incoming gradient, as the fused
+    towers do (engine.ScaledGrads). So its PEFT and input gradients are exactly linear in a
+    power-of-two scaling of dy (bit-exact at 2^-24, where an unscaled half backward would have
+    flushed the gradients to zero), and agree with the bf16 stack's within the 16-bit budget."""
+    from lcclip.adapter_clip import AdapterCLIP
+    from lcclip import freeze_backbone
+    from oracle import clip_oracle as o
+    sd = o.synthetic_state_dict(o.TINY, "adapter", "both", seed=21)
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(77, 3, o.TINY.transformer_width, device=dev, generator=g)
+    dy = torch.randn(x.shape, device=dev, generator=g) * 1e-4
+    res = {}
+    for prec, k in (("fp16", 0), ("fp16", -24), ("bf16", 0)):
+        w = AdapterCLIP.from_state_dict(sd, "adapter", "both", device=dev, text_precision=prec)
+        freeze_backbone(w)
+        w.train()
+        for m in w.modules():
+            if m.__class__.__name__ == "Adapter":
+                m.dropout = 0.0
+        xi = x.clone().requires_grad_(True)
+        y = w.model.transformer(xi)
+        (y * (dy * 2.0 ** k)).sum().backward()
+        peft = [p.grad * 2.0 ** -k for n, p in w.model.transformer.named_parameters()
+                if p.requires_grad]
+        res[(prec, k)] = (xi.grad * 2.0 ** -k, peft)
+    a, b, c = res[("fp16", 0)], res[("fp16", -24)], res[("bf16", 0)]
+    assert all(t.abs().sum() > 0 for t in a[1]) and a[0].abs().sum() > 0
+    assert torch.equal(a[0], b[0]) and all(torch.equal(u, v) for u, v in zip(a[1], b[1]))
+    assert rel(a[0], c[0]) < 2e-2
+    flat = lambda r: torch.cat([t.flatten() for t in r[1]])  # noqa: E731
+    assert rel(flat(a), flat(c)) < 4e-2

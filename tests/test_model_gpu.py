@@ -44,9 +44,9 @@ def record(**kw):
         f.write(json.dumps(kw) + "\n")
 
 
-def make_wrapper(sd, method, peft, dev, dropout=0.0):
+def make_wrapper(sd, method, peft, dev, dropout=0.0, image_precision="bf16"):
     from lcclip.adapter_clip import AdapterCLIP, set_adapter_dropout
-    w = AdapterCLIP.from_state_dict(sd, method, peft, device=dev)
+    w = AdapterCLIP.from_state_dict(sd, method, peft, device=dev, image_precision=image_precision)
     return set_adapter_dropout(w, dropout)
 
 
@@ -212,7 +212,7 @@ def test_vit_b16_full_shapes_vs_oracle(dev, method):
     check_logits(m)  # north star: logits within 1e-3 (cosine units, RMS)
 
 
-def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None):
+def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None, image_precision="bf16"):
     """One fused trainer fwd + CE-on-probs + bwd at ViT-B/16 shapes vs the oracle's train_step
     on the same weights: probs, loss, logits (tests/parity.py bounds) and every PEFT gradient.
     Gradients vs the fp32 oracle: the whole flat PEFT gradient rel-norm < GRAD_REL and every
@@ -224,7 +224,9 @@ def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None):
     same rounded algorithm that differ only in accumulation precision (fp32 vs fp64) are already
     5.0e-2 / 0.9848 apart (tools/summation_floor.py, profiles/r05/summation_floor.txt): the
     adapter down-projection gradients sum ~6k rows through relu kinks and cancel. The GPU is
-    held to that floor against the rounding oracle (measured 4.8e-2 / 0.9845) — DESIGN.md §2."""
+    held to that floor against the rounding oracle (measured 4.8e-2 / 0.9845) — DESIGN.md §2.
+    image_precision="fp16": the image tower at the reference's arithmetic (IEEE-half operands,
+    f32 residual stream); its rounding oracle is round_f16 on both towers."""
     from lcclip import OnlineTrainer
     cfg = o.VIT_B16
     sd = o.synthetic_state_dict(cfg, method, "both", seed=seed)
@@ -232,12 +234,13 @@ def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None):
     tok = o.synthetic_tokens(C, 77, seed=seed + 2)
     y = torch.arange(B) % C
     loss32, p32, i32, t32, g32, _ = o.train_step(img, tok, y, sd, cfg, method, "both")
-    g16 = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16,
+    rt_img = o.round_f16 if image_precision == "fp16" else o.round_bf16
+    g16 = o.train_step(img, tok, y, sd, cfg, method, "both", rt=rt_img,
                        rt_text=o.round_f16)[4]
     # the oracle that also rounds where the HIP backward stores bf16 gradients
     gfb = o.train_step(img, tok, y, sd, cfg, method, "both", rt=o.round_bf16_fwd_bwd,
-                       rt_text=o.round_f16_fwd_bwd)[4]
-    w = make_wrapper(sd, method, "both", dev)
+                       rt_text=o.round_f16_fwd_bwd)[4] if floor is not None else g16
+    w = make_wrapper(sd, method, "both", dev, image_precision=image_precision)
     with torch.no_grad():
         _, fi, ft = w(img.to(dev), tok.to(dev))
     tr = OnlineTrainer(w)
@@ -271,7 +274,7 @@ def _step_vs_oracle(dev, method, B, C, seed, tag, floor=None):
              fwdbwd_oracle_flat_rel_vs_fp32=rel(cat(gfb), cat(g32)),
              fwdbwd_oracle_cos_min_vs_fp32=min(cs(gfb[n], g32[n]) for n in g32),
              **logit_metrics(ls * fi.cpu() @ ft.cpu().t(), ls * i32 @ t32.t(), None, ls))
-    record(test=tag, method=method, B=B, C=C, **m)
+    record(test=tag, method=method, B=B, C=C, image_precision=image_precision, **m)
     assert m["probs_abs_vs_fp32"] < 1e-2 and m["loss_abs"] < 1e-2, m
     check_logits(m)
     if floor is None:
@@ -300,6 +303,60 @@ def test_adapter_config2_b32_step_vs_oracle(dev):
     """BASELINE config 2's method and prompt count (adapter both towers, C = 10) at B = 32: a
     larger batch than the B = 2 forward cases, the full train step against the oracle."""
     _step_vs_oracle(dev, "adapter", 32, 10, 81, "adapter_b32_c10_step", floor=(5.0e-2, 0.9848))
+
+
+def test_adapter_config2_fp16_image_step_vs_oracle(dev):
+    """Config 2's shape (adapter both towers, B = 32, C = 10) with the image tower at the
+    reference's own arithmetic (AdapterCLIP(image_precision="fp16"): the fp16 autocast of
+    methods/adapter_clip.py:87, IEEE-half operands, per-call power-of-two gradient scale): the
+    north-star gradient bound against the fp32 oracle with no summation-floor escape — flat
+    rel-norm < GRAD_REL and every tensor's cosine >= 0.99 — and the logits within 1e-3."""
+    _step_vs_oracle(dev, "adapter", 32, 10, 81, "adapter_b32_c10_step_fp16",
+                    image_precision="fp16")
+
+
+def test_lora_config1_fp16_image_step_vs_oracle(dev):
+    """Config 1's shape (LoRA both towers, B = 16, C = 16) with the fp16 image tower."""
+    _step_vs_oracle(dev, "lora", 16, 16, 61, "lora_b16_c16_step_fp16", image_precision="fp16")
+
+
+def test_fp16_image_tower_module_path_and_input_grad(golden, dev):
+    """The fp16 image tower through the module surface (AdapterCLIP.forward + autograd) gives
+    the fused trainer's PEFT gradients; and its stack-input gradient (need_dx, the scaled
+    backward's unscaling) matches the bf16 tower's within the 16-bit budget."""
+    from lcclip import OnlineTrainer, freeze_backbone
+    d, sd = golden
+    img = torch.from_numpy(d["images"]).to(dev)
+    tok = torch.from_numpy(d["tokens"]).to(dev)
+    y = torch.from_numpy(d["labels"]).to(dev)
+    w = make_wrapper(sd, "adapter", "both", dev, image_precision="fp16")
+    freeze_backbone(w)
+    w.train()
+    w.set_token(tok)
+    probs, _, _ = w(img)
+    torch.nn.functional.cross_entropy(probs, y).backward()
+    with torch.no_grad():
+        p16 = o.adapter_clip_forward(img.cpu(), tok.cpu(), method_sd(sd, "adapter"), o.TINY,
+                                     "adapter", "both", rt=o.round_f16, rt_text=o.round_f16)[0]
+    assert (probs.detach().cpu() - p16).abs().max() < 4e-3
+    w2 = make_wrapper(sd, "adapter", "both", dev, image_precision="fp16")
+    tr = OnlineTrainer(w2)
+    tr.forward_backward(img, y, tok)
+    n2 = dict(w2.model.named_parameters())
+    for n, p in w.model.named_parameters():
+        if p.requires_grad:
+            assert rel(p.grad, tr.grads[n2[n]]) < 1e-3, n
+    # input gradient of the tower (f32, unscaled) vs the bf16 tower's
+    gx = {}
+    for prec in ("fp16", "bf16"):
+        wi = make_wrapper(sd, "adapter", "both", dev, image_precision=prec)
+        tower = wi.model.visual.tower
+        f, ctx = tower.forward(img, save=True, training=True)
+        df = torch.randn(f.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+        grads = {p: torch.zeros(p.shape, device=dev) for p in tower.stack.trainable_params()}
+        gx[prec] = tower.backward(ctx, df * 1e-6, grads, need_dx=True).float().cpu()
+    assert gx["fp16"].abs().sum() > 0
+    assert rel(gx["fp16"], gx["bf16"]) < 2e-2
 
 
 def test_adapter_c100_step_vs_oracle(dev):
