@@ -124,6 +124,119 @@ class DataParallel:
         flat.mul_(1.0 / self.world)
 
 
+class ModuleDataParallel:
+    """One process per GPU for the autograd model surfaces (CLIP_MVP, BASELINE config 3; MaPLe,
+    config 5; AdapterCLIP's module path): the reference's single-process nn.DataParallel
+    (methods/_trainer.py:167-168) as one rank per GPU over RCCL.
+
+      * replicas: rank 0's parameters and buffers are broadcast once, at construction (the
+        one-time form of DataParallel's per-step replicate);
+      * the exposed class list: every rank contributes the classes of its share of the batch
+        and all ranks take the same merged list, in rank order, first occurrence kept — what the
+        reference's MVP trainer does with all_gather (methods/mvp_clip.py:300-313), so the logit
+        columns agree;
+      * gradients: after backward, the trainable parameters' gradients (MVP: key, mask,
+        g_prompts, e_prompts; MaPLe: the prompt learner) are all-reduced in flat buckets,
+        launched asynchronously one after another, and averaged — with equal per-rank batches
+        the gradient of the global-mean loss, which is what the reference's one loss over the
+        gathered outputs gives;
+      * per-batch statistics the modules keep (CLIP_MVP.count, mvp_clip.py:239-241) are summed
+        over ranks through `all_sum`, so every replica counts the global batch.
+    world == 1 (without LCCLIP_DP_FORCE) makes every call a no-op."""
+
+    def __init__(self, module, group=None, enabled=None, bucket_bytes=25 << 20):
+        self.module = module
+        self.dp = DataParallel(group, enabled)
+        self.bucket_bytes = int(bucket_bytes)
+        self.active = self.dp.active
+        if self.active:
+            tensors = [p.data for p in module.parameters()]
+            tensors += [b for b in module.buffers()
+                        if b.numel() and (b.is_floating_point() or b.dtype == torch.int64)]
+            self.dp.broadcast_from_root(tensors)
+            _invalidate_staging(module)
+        module._dp = self
+
+    @property
+    def world(self):
+        return self.dp.world
+
+    @property
+    def rank(self):
+        return self.dp.rank
+
+    def exposed_classes(self, local_classes):
+        """The global batch's class list from every rank's list (methods/mvp_clip.py:300-313)."""
+        local = [int(c) for c in local_classes]
+        if not self.active:
+            out = []
+        else:
+            parts = [None] * self.dp.world
+            dist.all_gather_object(parts, local, group=self.dp.group)
+            local = [c for part in parts for c in part]
+            out = []
+        for c in local:
+            if c not in out:
+                out.append(c)
+        return out
+
+    def all_sum(self, t):
+        """In-place SUM over ranks (blocking for the caller's stream)."""
+        if self.active:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.dp.group)
+        return t
+
+    def sync_grads(self):
+        """Average the trainable parameters' gradients over ranks (call after backward, before
+        the optimizer step)."""
+        if not self.active:
+            return
+        params = [p for p in self.module.parameters() if p.requires_grad]
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        groups = {}
+        for p in params:
+            groups.setdefault((p.grad.dtype, p.grad.device), []).append(p)
+        works = []
+        for ps in groups.values():
+            bucket, nbytes = [], 0
+            for p in ps + [None]:
+                if p is not None:
+                    bucket.append(p)
+                    nbytes += p.grad.numel() * p.grad.element_size()
+                if bucket and (p is None or nbytes >= self.bucket_bytes):
+                    flat = torch.cat([q.grad.reshape(-1) for q in bucket])
+                    works.append((dist.all_reduce(flat, op=dist.ReduceOp.SUM,
+                                                  group=self.dp.group, async_op=True),
+                                  flat, bucket))
+                    bucket, nbytes = [], 0
+        inv = 1.0 / self.dp.world
+        for w, flat, bucket in works:
+            w.wait()
+            flat.mul_(inv)
+            off = 0
+            for q in bucket:
+                q.grad.copy_(flat[off:off + q.numel()].view_as(q.grad))
+                off += q.numel()
+
+
+def _invalidate_staging(module):
+    """Drop every staged weight image under `module` (the tower engines re-stage from the
+    broadcast values; in-place collectives do not bump the tensors' version counters)."""
+    for m in module.modules():
+        eng = getattr(m, "_engine", None)
+        if eng is not None:
+            eng.invalidate_all()
+        for name in ("_tower", "_text_tower"):
+            t = getattr(m, name, None)
+            if t is not None:
+                t._key = None
+        cache = getattr(m, "_txt_cache", None)
+        if cache is not None:
+            cache.clear()
+
+
 def layer_ranges(stack, base: int = 0):
     """[(lo, hi)] offsets of each block's PEFT parameters inside a flat buffer whose layout is
     stack.trainable_params() in order, starting at `base`."""

@@ -11,11 +11,13 @@ learned context at rows 1..n_ctx, the image sequence gets proj(ctx) appended bef
 (L = 197 + n_ctx), and at layers 1..depth-1 the deep prompts overwrite those rows; backward
 returns the gradients of every prompt row through the frozen blocks.
 
-Deviations: compute is bf16 MFMA with fp32 accumulation and an fp32 residual stream (the
-reference casts the visual prompts to fp16, model.py:374 and :569). precision='fp8' (BASELINE
-config 5) runs the image tower's frozen QKV / c_fc / c_proj GEMMs, forward and input-gradient,
-as block-scaled e4m3 GEMMs on the fp8 MFMA (engine.BlockStack, precision attribute); the text
-tower (C x 77 rows: too few for the 256x256 fp8 tiles) stays bf16. Tokenisation needs a BPE
+Deviations: the image tower computes with bf16 MFMA operands and fp32 accumulation on the half
+residual stream (the reference casts the visual prompts to fp16, model.py:374 and :569); the
+text tower stores IEEE half (text_precision='fp16', the reference's dtype; 'bf16' optional).
+precision='fp8' (BASELINE config 5) runs the image tower's frozen QKV / c_fc / c_proj GEMMs,
+forward and input-gradient, as block-scaled e4m3 GEMMs on the fp8 MFMA (engine.BlockStack,
+precision attribute); the text tower (C x 77 rows: too few for the 256x256 fp8 tiles) keeps its
+16-bit storage. Tokenisation needs a BPE
 tokenizer callable (tokenizer=); without one, set_tokenized_prompts() takes token ids and the
 context is initialised from the reference's random branch (maple.py:95-98), or from
 ctx_init_tokens (the ids of "a bad photo of a") as its ctx_init branch does.
@@ -122,7 +124,8 @@ class MaPLe(nn.Module):
     """maple.py:143-253."""
 
     def __init__(self, model_name="ViT-B/16", n_ctx=3, device="cpu", tokenizer=None,
-                 ctx_init_tokens=None, arch_overrides=None, clip_model=None, precision="bf16"):
+                 ctx_init_tokens=None, arch_overrides=None, clip_model=None, precision="bf16",
+                 text_precision="fp16"):
         super().__init__()
         self.device = device
         if clip_model is None:
@@ -147,6 +150,7 @@ class MaPLe(nn.Module):
         self.current_class_names = []
         self.prompt_prefix = self.prompt_learner.prompt_prefix
         self.set_precision(precision)
+        self.set_text_precision(text_precision)
         if device is not None and str(device) != "cpu":
             self.to(device)
 
@@ -156,6 +160,18 @@ class MaPLe(nn.Module):
             raise ValueError("precision must be 'bf16' or 'fp8'")
         self.precision = precision
         self.image_encoder.tower.stack.precision = precision
+        return self
+
+    def set_text_precision(self, precision):
+        """The text tower's 16-bit storage: 'fp16' (default; IEEE half, the reference's own
+        MaPLe backbone dtype, maple_clip/model.py:749-772, 826) or 'bf16'. Its backward runs on
+        a per-call power-of-two gradient scale (engine.ScaledGrads) and returns the deep-prompt
+        and context-embedding gradients unscaled."""
+        dt = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(precision)
+        if dt is None:
+            raise ValueError("text_precision must be 'fp16' or 'bf16'")
+        self.base_clip_model.transformer.engine.set_storage(dt)
+        self.text_precision = precision
         return self
 
     @classmethod

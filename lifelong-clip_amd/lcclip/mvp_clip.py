@@ -66,7 +66,7 @@ class CLIP_MVP(nn.Module):
                  num_classes: int = 100, lambd: float = 1.0, use_mask: bool = True,
                  use_contrastiv: bool = False, use_last_layer: bool = True,
                  model_name="ViT-B/16", device="cpu", tokenizer=None, arch_overrides=None,
-                 backbone=None, **kwargs):
+                 backbone=None, text_precision="fp16", **kwargs):
         super().__init__()
         self.features = torch.empty(0)
         self.keys = torch.empty(0)
@@ -119,6 +119,13 @@ class CLIP_MVP(nn.Module):
         self.e_prompts = nn.Parameter(torch.randn(e_pool, self.e_size, embed_dim))
         self.exposed_classes = 0
         self._txt_cache = TokenFeatureCache()
+        # the frozen text tower's 16-bit storage: IEEE half, the reference's autocast dtype
+        # ('bf16' optional); forward only, its features cached
+        dt = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(text_precision)
+        if dt is None:
+            raise ValueError("text_precision must be 'fp16' or 'bf16'")
+        self.backbone.transformer.engine.set_storage(dt)
+        self.text_precision = text_precision
         if device is not None and str(device) != "cpu":
             self.to(device)
 
@@ -237,6 +244,9 @@ class CLIP_MVP(nn.Module):
         if self.training:
             with torch.no_grad():
                 num = topk.view(-1).bincount(minlength=self.e_prompts.size(0))
+                dp = getattr(self, "_dp", None)
+                if dp is not None:  # one rank per GPU: count the global batch on every replica
+                    dp.all_sum(num)
                 self.count += num
         if e_prompts.dim() == 2:  # B == 1: the reference's squeeze() dropped the batch axis
             e_prompts = e_prompts.unsqueeze(0)

@@ -975,12 +975,14 @@ def mvp_prompt_layers(g_prompt, e_prompt, pos_g, len_g, pos_e, len_e, n_layers):
 
 
 def mvp_forward(img, tokens, p, cfg: ClipConfig, mvp: dict, pos_g=(0, 1), len_g=5,
-                pos_e=(2, 3, 4), len_e=20, use_last_layer=True, use_mask=True, rt=identity):
+                pos_e=(2, 3, 4), len_e=20, use_last_layer=True, use_mask=True, rt=identity,
+                rt_text=None):
     """CLIP_MVP.forward (mvp_clip.py:282-288) over forward_features (:182-264) and forward_head
     (:266-280), prompt_func 'prompt_tuning', selection_size 1, use_contrastiv False.
     mvp: {'key' [pool, W], 'mask' [pool, n_classes], 'g_prompts' [1, G, W], 'e_prompts'
     [pool, E, W]}. Returns (logits [B, C] (masked when use_mask), similarity_loss, image
-    features [B, E], text features [C, E], mask [B, C], topk [B, 1])."""
+    features [B, E], text features [C, E], mask [B, C], topk [B, 1]). rt_text: the text
+    tower's rounding when it differs from the image tower's (the IEEE-half text tower)."""
     vis, _ = tower_prefixes(cfg)
     xr = prompt_tower_resid(cfg, rt)
     x0 = xr(mvp_embed(img, p, cfg, rt))
@@ -1007,7 +1009,8 @@ def mvp_forward(img, tokens, p, cfg: ClipConfig, mvp: dict, pos_g=(0, 1), len_g=
         x = x[:, :N]
     x = rt(layer_norm(x[:, 0, :], p["visual.ln_post.weight"], p["visual.ln_post.bias"]))
     img_f = linear(x, p["visual.proj"].t(), None, rt)                          # :259-261
-    txt_f = encode_text(tokens, p, cfg, "vanilla", "none", rt)                   # :192
+    txt_f = encode_text(tokens, p, cfg, "vanilla", "none",
+                        rt if rt_text is None else rt_text)                     # :192
     C = tokens.shape[0]
     mask = torch.sigmoid(mask) * 2.0                                           # :263
     logits, _, _ = clip_logits(img_f, txt_f, p["logit_scale"])                 # :266-280

@@ -218,3 +218,63 @@ def test_trainer_replicates_rank0_once(WORLD):
         assert torch.equal(outs[r]["flat_p"], outs[0]["flat_p"])
     for k, v in r0.items():
         assert torch.equal(outs[0]["after"][k], v), k  # rank 0 keeps its own
+
+
+def _module_dp_worker(rank, port, tmpdir, WORLD):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    from lcclip.dp import ModuleDataParallel
+    torch.manual_seed(100 + rank)  # rank-dependent init: replication must fix it
+    net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+    net.register_buffer("count", torch.zeros(3))
+    net[0].bias.requires_grad_(False)  # a frozen parameter is replicated but not averaged
+    ddp = ModuleDataParallel(net)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4 * WORLD, 6, generator=g)
+    y = torch.randint(0, 3, (4 * WORLD,), generator=g)
+    sl = slice(rank * 4, (rank + 1) * 4)
+    loss = torch.nn.functional.cross_entropy(net(x[sl]), y[sl])
+    loss.backward()
+    ddp.sync_grads()
+    num = y[sl].bincount(minlength=3).float()
+    net.count += ddp.all_sum(num)
+    classes = ddp.exposed_classes([int(c) for c in y[sl]][::-1])
+    torch.save({"state": {k: v.clone() for k, v in net.state_dict().items()},
+                "grads": {n: p.grad.clone() for n, p in net.named_parameters() if p.grad is not None},
+                "classes": classes}, os.path.join(tmpdir, f"m{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("WORLD", [2, 4])
+def test_module_data_parallel(WORLD):
+    """lcclip.dp.ModuleDataParallel (the autograd surfaces' DDP, MVP / MaPLe): rank 0's weights
+    and buffers replicated at construction, trainable gradients averaged to the global-batch
+    gradient, per-batch counts summed, and the exposed-class list merged in rank order with the
+    first occurrence kept (methods/mvp_clip.py:300-313)."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_module_dp_worker, args=(_free_port(), tmp, WORLD), nprocs=WORLD, join=True)
+        outs = [torch.load(os.path.join(tmp, f"m{r}.pt"), weights_only=True) for r in range(WORLD)]
+    # single process, global batch, rank 0's initial weights
+    torch.manual_seed(100)
+    net = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+    net[0].bias.requires_grad_(False)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4 * WORLD, 6, generator=g)
+    y = torch.randint(0, 3, (4 * WORLD,), generator=g)
+    torch.nn.functional.cross_entropy(net(x), y).backward()
+    for r in range(WORLD):
+        for n, p in net.named_parameters():
+            if p.requires_grad:
+                assert torch.allclose(outs[r]["grads"][n], p.grad, atol=1e-6), (r, n)
+            else:
+                assert n not in outs[r]["grads"]
+        for k, v in net.state_dict().items():
+            assert torch.equal(outs[r]["state"][k], v), (r, k)
+        assert torch.equal(outs[r]["state"]["count"], y.bincount(minlength=3).float())
+    want = []
+    for r in range(WORLD):
+        for c in [int(c) for c in y[r * 4:(r + 1) * 4]][::-1]:
+            if c not in want:
+                want.append(c)
+    assert all(o_["classes"] == want for o_ in outs)

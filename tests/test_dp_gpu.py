@@ -179,3 +179,96 @@ def test_trainer_dp_replicas_identical_after_step(dev, method):
     assert up_ref.abs().sum() > 0
     agree = (torch.sign(up) == torch.sign(up_ref)).float().mean().item()
     assert agree > 0.95, agree
+
+
+# ---------------------------------------------------------------- MVP / MaPLe (configs 3, 5)
+def _prompt_model(kind, rank=0):
+    """A TINY CLIP_MVP or MaPLe on cuda:0 with the oracle's synthetic weights (rank != 0: other
+    random prompt parameters, which the replication must overwrite)."""
+    _path()
+    from oracle import clip_oracle as o
+    dev = torch.device("cuda:0")
+    if kind == "mvp":
+        from lcclip.mvp_clip import CLIP_MVP
+        cfg = o.TINY_MVP
+        sd = o.synthetic_state_dict(cfg, seed=21)
+        mv = o.mvp_params(cfg, seed=3 + rank)
+        m = CLIP_MVP.from_state_dict(sd, device=dev, num_classes=mv["mask"].shape[1],
+                                     task_num=mv["key"].shape[0])
+        with torch.no_grad():
+            for k in ("key", "mask", "g_prompts", "e_prompts"):
+                getattr(m, k).copy_(mv[k])
+    else:
+        from lcclip.maple import MaPLe
+        cfg = o.TINY_MAPLE
+        sd = o.synthetic_state_dict(cfg, seed=41)
+        mp_ = o.maple_params(cfg, seed=2 + rank)
+        m = MaPLe.from_state_dict(sd, device=dev)
+        params = dict(m.named_parameters())
+        with torch.no_grad():
+            for k, name in o.MAPLE_TO_MODULE.items():
+                params[name].copy_(mp_[k])
+    B, C = 4, 4
+    img = o.synthetic_images(B, cfg.image_resolution, seed=5).to(dev)
+    tok = o.synthetic_tokens(C, cfg.context_length, seed=5, vocab=cfg.vocab_size).to(dev)
+    y = torch.tensor([0, 3, 1, 2], device=dev)
+    return m, img, tok, y
+
+
+def _prompt_step(kind, m, img, tok, y):
+    m.train()
+    if kind == "mvp":
+        m.text_tokens = tok
+        logits = m(img, tok)
+        loss = m.loss_fn(logits, y)
+    else:
+        m.set_tokenized_prompts(tok)
+        loss = torch.nn.functional.cross_entropy(m(img), y)
+    loss.backward()
+
+
+def _worker_prompt(rank, world, port, tmpdir, kind):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from lcclip.dp import ModuleDataParallel
+    m, img, tok, y = _prompt_model(kind, rank)
+    ddp = ModuleDataParallel(m)
+    per = img.shape[0] // world
+    sl = slice(rank * per, (rank + 1) * per)
+    # every rank derives the same class list from the global batch's labels
+    classes = ddp.exposed_classes(y[sl].tolist())
+    _prompt_step(kind, m, img[sl], tok, y[sl])
+    ddp.sync_grads()
+    torch.cuda.synchronize()
+    out = {"grads": {n: p.grad.cpu() for n, p in m.named_parameters() if p.requires_grad},
+           "classes": classes}
+    if kind == "mvp":
+        out["count"] = m.count.cpu()
+    torch.save(out, os.path.join(tmpdir, f"p{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["mvp", "maple"])
+def test_prompt_models_dp_match_global_batch(dev, kind):
+    """verdict r5: the DDP exchange of MVP (config 3) and MaPLe (config 5). Two ranks share the
+    GPU over gloo, each with half of the batch and (rank 1) other initial prompt parameters;
+    after ModuleDataParallel's replication, the global class list and the averaged gradient
+    all-reduce they hold the single-process global-batch gradients of every trainable tensor
+    (MVP: key, mask, g / e prompts; MaPLe: the prompt learner) and, for MVP, its global counts."""
+    m, img, tok, y = _prompt_model(kind)
+    _prompt_step(kind, m, img, tok, y)
+    torch.cuda.synchronize()
+    ref = {n: p.grad.cpu() for n, p in m.named_parameters() if p.requires_grad}
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker_prompt, args=(world, _free_port(), tmp, kind), nprocs=world, join=True)
+        outs = [torch.load(os.path.join(tmp, f"p{r}.pt"), weights_only=True) for r in range(world)]
+    for n, g in ref.items():
+        assert torch.equal(outs[0]["grads"][n], outs[1]["grads"][n]), n
+        err = ((outs[0]["grads"][n] - g).norm() / g.norm().clamp_min(1e-30)).item()
+        assert err < 2e-2, (n, err)
+    assert outs[0]["classes"] == outs[1]["classes"] == list(dict.fromkeys(y.tolist()))
+    if kind == "mvp":
+        assert torch.equal(outs[0]["count"], m.count.cpu())
+        assert torch.equal(outs[1]["count"], m.count.cpu())

@@ -65,7 +65,8 @@ def test_mvp_tiny_forward_and_grads(dev, use_last_layer):
         l32, s32, i32, t32, m32, k32 = o.mvp_forward(img, tok, sd, cfg, mv,
                                                      use_last_layer=use_last_layer)
         l16, s16, *_ , k16 = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=use_last_layer,
-                                           rt=o.round_bf16)
+                                           rt=o.round_bf16,
+                                           rt_text=o.round_f16)
     loss_ref, g_ref = oracle_grads(img, tok, y, sd, cfg, mv, use_last_layer=use_last_layer)
 
     m = build(cfg, sd, mv, dev, use_last_layer=use_last_layer)
@@ -134,7 +135,8 @@ def test_mvp_vit_b16_shapes(dev):
     y = torch.tensor([1, 2])
     with torch.no_grad():
         l32, s32, *_ = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=False)
-        l16, *_ = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=False, rt=o.round_bf16)
+        l16, *_ = o.mvp_forward(img, tok, sd, cfg, mv, use_last_layer=False, rt=o.round_bf16,
+                                           rt_text=o.round_f16)
     _, g_ref = oracle_grads(img, tok, y, sd, cfg, mv, use_last_layer=False)
     m = build(cfg, sd, mv, dev, use_last_layer=False)
     m.text_tokens = tok.to(dev)
@@ -174,7 +176,8 @@ def test_mvp_config3_shape_vs_oracle(dev):
     with torch.no_grad():
         logits = m(img.to(dev)).float().cpu()
         l32, *_ = o.mvp_forward(img[pick], tok, sd, cfg, mv, use_last_layer=False)
-        l16, *_ = o.mvp_forward(img[pick], tok, sd, cfg, mv, use_last_layer=False, rt=o.round_bf16)
+        l16, *_ = o.mvp_forward(img[pick], tok, sd, cfg, mv, use_last_layer=False, rt=o.round_bf16,
+                                           rt_text=o.round_f16)
     ls = math.exp(sd["logit_scale"].item())
     met = logit_metrics(logits[pick], l32, None, ls)
     met["cos_max_vs_bf16"], met["cos_rms_vs_bf16"] = logit_errors(logits[pick], l16, ls)
