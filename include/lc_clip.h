@@ -192,7 +192,8 @@ int lc_vit_embed_ln_x16(hipStream_t stream, int n_img, int n_patch, int D, const
 /* lc_layernorm_bwd_x16 with the residual gradient in IEEE half as well: dres and dx half
  * [rows, ldo] (ldo % 4 == 0, 8-B aligned), the gradient carrying a power-of-two scale set
  * upstream (lc_grad_pow2_normalize: the reference's GradScaler, methods/adapter_clip.py:93);
- * dx_bf16 is the bf16 copy of the stored half value. */
+ * dx_bf16 is the bf16 copy of the stored half value, or NULL (the adapter tower: its
+ * consumers read the half gradient directly, lc_adapter_bwd_g16 / _wgrad_ws_unscaled_g16). */
 int lc_layernorm_bwd_g16(hipStream_t stream, int rows, int D, const void* dy, int dy_f32,
                          long ldy, const void* x, long ldx, const float* mean, const float* rstd,
                          const float* gamma, const void* dres, void* dx, void* dx_bf16,
@@ -203,6 +204,20 @@ int lc_adapter_wgrad_ws_unscaled(hipStream_t stream, int M, int D, const void* g
                                  const void* h, const void* z, long ldz, const void* dpre,
                                  float scale, float* dWu, float* dbu, float* dWd, float* dbd,
                                  void* ws, long ws_bytes, const float* gscale);
+/* The two adapter backward launches reading the half residual gradient itself: gout IEEE half
+ * [M, ldg] (16-B aligned), every other 16-bit operand bf16. Each gout value enters as its bf16
+ * rounding, the value lc_layernorm_bwd_g16's dx_bf16 copy holds, so the results equal
+ * lc_adapter_bwd / lc_adapter_wgrad_ws_unscaled on that copy bit for bit, without it being
+ * written (77 MB per LayerNorm backward at ViT-B/16 B = 256). lc_adapter_bwd_g16: D = 512 or
+ * 768, any M, dz may be NULL (dpre only). Replaces: adapter.py:59-72 autograd, as lc_adapter_bwd
+ * and lc_adapter_wgrad. */
+int lc_adapter_bwd_g16(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
+                       const void* WuT, const void* WdT, float scale, float keep, void* dpre,
+                       void* dz, long ldz);
+int lc_adapter_wgrad_ws_unscaled_g16(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                                     const void* h, const void* z, long ldz, const void* dpre,
+                                     float scale, float* dWu, float* dbu, float* dWd, float* dbd,
+                                     void* ws, long ws_bytes, const float* gscale);
 int lc_adapter_ln_fwd_x16(hipStream_t stream, int M, int D, const void* z, long ldz,
                           const void* Wd, const float* bd, const void* Wu, const float* bu,
                           float scale, float keep, unsigned long long seed,
@@ -259,6 +274,11 @@ int lc_attn_fwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, lo
 int lc_attn_bwd(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
                 const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
                 int causal);
+/* Testing / A-B: the kernel form lc_attn_bwd uses (process-wide): 0 automatic (default),
+ * 1 fused single pass (dS^T parked in LDS), 2 key-major + query-major kernel pair, 3 two-phase
+ * (dQ, then dK / dV, in one workgroup with 59 KB of LDS: two workgroups per CU; L <= 224).
+ * All forms compute the same dq|dk|dv up to f32 summation order. -1 for other values. */
+int lc_attn_bwd_set_form(int form);
 /* The backward with dq|dk|dv written as the A operand of the fp8 QKV input-gradient GEMM
  * (lc_gemm_nt_fp8): e4m3 codes dqkv [n_seq*L, lddq BYTES] (lddq % 16 == 0, 16-B aligned) + E8M0
  * scales q_scale [3*H*64/128][q_rows][4] (q_rows = n_seq*L rounded up to 256), bit-identical to
@@ -507,6 +527,7 @@ int lc_attn_fwd_f16(hipStream_t stream, int n_seq, int L, int H, const void* qkv
 int lc_attn_bwd_f16(hipStream_t stream, int n_seq, int L, int H, const void* qkv, long ldq,
                     const void* O, const void* dO, long ldo, const float* lse, void* dqkv, long lddq,
                     int causal);
+int lc_attn_bwd_set_form_f16(int form);
 int lc_cast_bf16_f16(hipStream_t stream, long n, const float* src, void* dst);
 int lc_merge_weight_f16(hipStream_t stream, int N, int K, int r, const float* W, const float* A,
                         const float* B, float scaling, void* out, void* outT);

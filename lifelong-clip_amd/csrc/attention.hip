@@ -935,6 +935,288 @@ attn_bwd_q_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   }
 }
 
+// ------------------------------------------------ backward, two-phase (dQ, then dK / dV), 2 per CU
+// One workgroup per (sequence, head), NQB waves; wave w owns the 16-row blocks w and w + NQB
+// (its queries in phase 1, its keys in phase 2). LDS holds one pair of row images at a time
+// (K | V, then Q | dO) plus the -lse / -D rows: 59 KB at L <= 224, so two workgroups share a CU
+// and one's loads and stores run under the other's MFMA / exp chain. The fused kernel parks
+// the whole dS^T (163 KB: one workgroup per CU, 1.75 waves per SIMD, its memory instructions
+// exposed: profiles/r03/j_attn_bwd_knockouts.txt). The price is S and dP formed twice.
+//   phase 1 (query-major, attn_bwd_q_kernel's math): S^T = K Q^T, dP^T = V dO^T - D from the
+//     K / V images and the wave's Q / dO fragments; dQ^T += K^T dS^T.
+//   hand-over: each wave reads its key blocks' K / V fragments from the images, then writes its
+//     query blocks' Q / dO fragments as the Q / dO images (every row is one wave's block).
+//   phase 2 (key-major, attn_bwd_kv_kernel's math on 16-key blocks): S = Q K^T,
+//     dP = dO V^T - D; dV^T += dO^T P, dK^T += Q^T dS.
+template <int NQB, bool CAUSAL>
+__global__ void __launch_bounds__(64 * NQB) __attribute__((amdgpu_waves_per_eu(4)))
+attn_bwd2_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
+                 const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, long ldo,
+                 const float* __restrict__ lse, bf16_t* __restrict__ dqkv, long lddq, float scale,
+                 int ko) {
+  constexpr int causal = CAUSAL;
+  // non-causal: both query / key chunk loops fully unrolled (LDS offsets in the instructions,
+  // the edge chunk known at compile time); causal: runtime bounds, rolled
+  constexpr int UNR = CAUSAL ? 1 : NQB;
+  // ko: timing knockouts of DIAG builds (LC_ATT2_KO; results wrong), 0 otherwise: 1 no phase-1
+  // loop, 2 no phase-2 loop, 4 stores replaced by keep-alives, 8 every item loads item 0's rows
+  constexpr int LP = 32 * NQB;
+  constexpr int NTH = 64 * NQB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * LP * 128 + 2 * LP * 4];
+  char* I0 = smem;             // K rows, then Q rows
+  char* I1 = smem + LP * 128;  // V rows, then dO rows
+  float* nlse_s = reinterpret_cast<float*>(smem + 2 * LP * 128);  // -lse
+  float* nd_s = nlse_s + LP;                                       // -D
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar block bounds
+  const int g = lane >> 4, t = lane & 15;
+  const int nh = blockIdx.x, n = nh / H, h = nh % H;
+  const long base = (long)n * L;
+  const float c = scale * LOG2E;
+
+  // every global load first, through raw-buffer descriptors over this sequence's L rows (rows
+  // >= L read zeros from the range check: no branch around a load, so no vmcnt(0) between them):
+  // K / V rows for the images, then the wave's two query blocks' Q / dO fragments (B operands
+  // of S^T / dP^T: lane holds row q = qb + t, columns s*32 + 8g ..), O rows and lse
+  auto rows_rsrc = [&](const void* p, long row0, long row_bytes) {
+    const uint64_t a = (uint64_t)(static_cast<const char*>(p) + row0 * row_bytes);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)(L * row_bytes));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+  };
+  auto bld16 = [](__amdgpu_buffer_rsrc_t r, int off) {  // nontemporal (read once)
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
+  const long lb = (ko & 8) ? 0 : base;
+  const int hl = (ko & 8) ? 0 : h;
+  const auto rq = rows_rsrc(qkv, lb, ldq * 2);
+  const auto rd = rows_rsrc(dO, lb, ldo * 2);
+  const auto rO = rows_rsrc(O, lb, ldo * 2);
+  const auto rl = rows_rsrc(lse, (ko & 8) ? 0 : (long)nh * L, 4);
+  constexpr int IT = LP * 8 / NTH;  // = 4
+  const int ch = tid & 7;
+  uint4 kv[IT], vv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    const int off = r * (int)ldq * 2 + (hl * 64 + ch * 8) * 2;
+    kv[i] = bld16(rq, off + D * 2);
+    vv[i] = bld16(rq, off + D * 4);
+  }
+  bf16x8 qf[2][2], df[2][2];
+  uint4 of[2][2];
+  float lv[2];
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int q = 16 * (w + NQB * bk) + t;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int cb = (hl * 64 + s * 32 + g * 8) * 2;
+      uint4 u = bld16(rq, q * (int)ldq * 2 + cb);
+      uint4 d = bld16(rd, q * (int)ldo * 2 + cb);
+      of[bk][s] = bld16(rO, q * (int)ldo * 2 + cb);
+      qf[bk][s] = *reinterpret_cast<bf16x8*>(&u);
+      df[bk][s] = *reinterpret_cast<bf16x8*>(&d);
+    }
+    lv[bk] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, q * 4, 0, 0));
+    asm volatile("" : "+v"(lv[bk]));  // issued here, not sunk into the q < L select below
+  }
+  float nl[2], nd[2];
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int q = 16 * (w + NQB * bk) + t;
+    float dsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 d8 = df[bk][s];
+      const u32x4 dd = __builtin_bit_cast(u32x4, d8);
+      const uint32_t oo[4] = {of[bk][s].x, of[bk][s].y, of[bk][s].z, of[bk][s].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        dsum += bf2f(oo[k] & 0xffff) * bf2f(dd[k] & 0xffff) + bf2f(oo[k] >> 16) * bf2f(dd[k] >> 16);
+    }
+    dsum += __shfl_xor(dsum, 16);
+    dsum += __shfl_xor(dsum, 32);
+    nd[bk] = -dsum;
+    nl[bk] = q < L ? -lv[bk] : -1e30f;
+    if (g == 0) {  // phase 2 reads every query's -lse / -D from LDS
+      nd_s[q] = nd[bk];
+      nlse_s[q] = nl[bk];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int r = (tid + i * NTH) >> 3;
+    *reinterpret_cast<uint4*>(I0 + r * 128 + swz(r, ch) * 16) = kv[i];
+    *reinterpret_cast<uint4*>(I1 + r * 128 + swz(r, ch) * 16) = vv[i];
+  }
+  __syncthreads();
+
+  const int ro0 = row_off(t, g, 0), ro1 = row_off(t, g, 1);
+  const int tro[4] = {tr_off(t, g, 0), tr_off(t, g, 1), tr_off(t, g, 2), tr_off(t, g, 3)};
+
+  // ---- phase 1: dQ of the wave's query blocks
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int qb = 16 * (w + NQB * bk);
+    if (qb >= L) continue;  // wave-uniform
+    const int s_end = (ko & 1) ? 0 : causal ? (qb + 15) / 32 + 1 : NQB;
+    f32x4 dQ[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dQ[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll UNR
+    for (int s = 0; s < NQB; ++s) {
+      if (s >= s_end) break;
+      const bool edge = (32 * s + 32 > L) || (causal && 32 * s + 31 > qb);
+      // one 16-key tile of S^T / dP^T live at a time, packed to bf16 straight away; k slots of
+      // the dS^T operand: j < 4 -> key 32s + 4g + j, j >= 4 -> 32s + 16 + 4g + (j - 4)
+      u32x4 sw;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ro = (32 * s + 16 * kk) * 128;
+        const bf16x8 ka0 = lds16(I0 + ro + ro0), ka1 = lds16(I0 + ro + ro1);
+        const bf16x8 va0 = lds16(I1 + ro + ro0), va1 = lds16(I1 + ro + ro1);
+        f32x4 S = mfma16(ka0, qf[bk][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S = mfma16(ka1, qf[bk][1], S);
+        f32x4 dP = mfma16(va0, df[bk][0], f32x4{nd[bk], nd[bk], nd[bk], nd[bk]});
+        dP = mfma16(va1, df[bk][1], dP);
+        // lane holds X^T[key = 32s + 16kk + 4g + r][q = qb + t]
+        f32x4 p;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = ex2(__builtin_fmaf(S[r], c, nl[bk]));
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            p[r] = masked(32 * s + 16 * kk + 4 * g + r, qb + t, L, causal) ? 0.f : p[r];
+        }
+        const f32x4 ds = p * dP;
+        sw[2 * kk] = pack2bf(ds[0], ds[1]);
+        sw[2 * kk + 1] = pack2bf(ds[2], ds[3]);
+      }
+      const bf16x8 sb = as_bf8(sw);
+      const char* kblk = I0 + 32 * s * 128;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 kT = cat4(lds_tr(kblk + tro[dt]), lds_tr(kblk + 16 * 128 + tro[dt]));
+        dQ[dt] = mfma16(kT, sb, dQ[dt]);
+      }
+    }
+    // lane holds dQ^T[d = dt*16 + 4g + r][q = qb + t]
+    const int q = qb + t;
+    if (q < L) {  // the 4 lanes of the row agree
+      uint2 x[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        x[dt] = uint2{pack2bf(dQ[dt][0] * scale, dQ[dt][1] * scale),
+                      pack2bf(dQ[dt][2] * scale, dQ[dt][3] * scale)};
+      if (ko & 4)
+        asm volatile("" ::"v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]));
+      else
+        store_row64(dqkv + (base + q) * lddq + h * 64, g, x);
+    }
+  }
+
+  // ---- hand-over: K / V fragments of the wave's key blocks (B operands of S = Q K^T,
+  // dP = dO V^T: lane holds row key = kb + t, columns s*32 + 8g ..), then the Q / dO images
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int kb = 16 * (w + NQB * bk);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kf[bk][s] = lds16(I0 + kb * 128 + (s ? ro1 : ro0));
+      vf[bk][s] = lds16(I1 + kb * 128 + (s ? ro1 : ro0));
+    }
+  }
+  __syncthreads();  // every wave holds its K / V fragments
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int qb = 16 * (w + NQB * bk);  // rows >= L: zeros (loaded so)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      *reinterpret_cast<bf16x8*>(I0 + qb * 128 + (s ? ro1 : ro0)) = qf[bk][s];
+      *reinterpret_cast<bf16x8*>(I1 + qb * 128 + (s ? ro1 : ro0)) = df[bk][s];
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: dK, dV of the wave's key blocks
+#pragma unroll
+  for (int bk = 0; bk < 2; ++bk) {
+    const int kb = 16 * (w + NQB * bk);
+    if (kb >= L) continue;  // wave-uniform
+    f32x4 dV[4], dK[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dV[dt] = dK[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int qc0 = (ko & 2) ? NQB : causal ? kb / 32 : 0;  // (causal: earlier queries see none of it)
+#pragma unroll UNR
+    for (int qc = 0; qc < NQB; ++qc) {
+      if (qc < qc0) continue;
+      const bool edge = (kb + 16 > L) || (causal && kb + 15 > qc * 32);
+      // k slots of the P / dS operands: j < 4 -> q = 32qc + 4g + j, j >= 4 -> 32qc + 16 + 4g + j-4
+      u32x4 pw, sw;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int q0 = qc * 32 + qt * 16 + 4 * g;
+        const f32x4 nlv = *reinterpret_cast<const f32x4*>(nlse_s + q0);
+        const f32x4 ndv = *reinterpret_cast<const f32x4*>(nd_s + q0);
+        const int ro = (qc * 32 + qt * 16) * 128;
+        const bf16x8 qa0 = lds16(I0 + ro + ro0), qa1 = lds16(I0 + ro + ro1);
+        const bf16x8 da0 = lds16(I1 + ro + ro0), da1 = lds16(I1 + ro + ro1);
+        f32x4 S = mfma16(qa0, kf[bk][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        S = mfma16(qa1, kf[bk][1], S);
+        f32x4 dP = mfma16(da0, vf[bk][0], ndv);
+        dP = mfma16(da1, vf[bk][1], dP);
+        // lane holds X[q = q0 + r][key = kb + t]
+        f32x4 p;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) p[r] = ex2(__builtin_fmaf(S[r], c, nlv[r]));
+        if (edge) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[r] = masked(kb + t, q0 + r, L, causal) ? 0.f : p[r];
+        }
+        const f32x4 ds = p * dP;
+        pw[2 * qt] = pack2bf(p[0], p[1]);
+        pw[2 * qt + 1] = pack2bf(p[2], p[3]);
+        sw[2 * qt] = pack2bf(ds[0], ds[1]);
+        sw[2 * qt + 1] = pack2bf(ds[2], ds[3]);
+      }
+      const bf16x8 pB = as_bf8(pw), sB = as_bf8(sw);
+      const char* qblk = I0 + qc * 32 * 128;
+      const char* dblk = I1 + qc * 32 * 128;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 doT = cat4(lds_tr(dblk + tro[dt]), lds_tr(dblk + 16 * 128 + tro[dt]));
+        const bf16x8 qT = cat4(lds_tr(qblk + tro[dt]), lds_tr(qblk + 16 * 128 + tro[dt]));
+        dV[dt] = mfma16(doT, pB, dV[dt]);
+        dK[dt] = mfma16(qT, sB, dK[dt]);
+      }
+    }
+    // lane holds X^T[d = dt*16 + 4g + r][key = kb + t]
+    const int key = kb + t;
+    if (key < L) {
+      uint2 xk[4], xv[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        xk[dt] = uint2{pack2bf(dK[dt][0] * scale, dK[dt][1] * scale),
+                       pack2bf(dK[dt][2] * scale, dK[dt][3] * scale)};
+        xv[dt] = uint2{pack2bf(dV[dt][0], dV[dt][1]), pack2bf(dV[dt][2], dV[dt][3])};
+      }
+      bf16_t* dst = dqkv + (base + key) * lddq + h * 64;
+      if (ko & 4) {
+        asm volatile("" ::"v"(xk[0]), "v"(xk[1]), "v"(xk[2]), "v"(xk[3]));
+        asm volatile("" ::"v"(xv[0]), "v"(xv[1]), "v"(xv[2]), "v"(xv[3]));
+      } else {
+        store_row64(dst + D, g, xk);
+        store_row64(dst + 2 * D, g, xv);
+      }
+    }
+  }
+}
+
 // workgroups of a persistent launch: as many as fit on the chip at once (LDS-limited) when there
 // are many items per workgroup (L = 197: 3072 items, 12 per workgroup), else one per item
 int persistent_grid(int items, int lds_bytes) {
@@ -952,6 +1234,19 @@ int persistent_grid(int items, int lds_bytes) {
   // a few items per workgroup would leave a ragged last round: one item each (no pipelining)
   return items < 4 * g ? items : g;
 }
+
+// lc_attn_bwd_set_form: 0 automatic, else one of these
+enum { ATTN_BWD_FUSED = 1, ATTN_BWD_SPLIT = 2, ATTN_BWD_TWO_PHASE = 3 };
+const int g_att2_ko = [] {  // DIAG builds: attn_bwd2_kernel timing knockouts
+  const char* e = lc_diag_env("LC_ATT2_KO");
+  return e ? atoi(e) : 0;
+}();
+int g_attn_bwd_form = [] {  // DIAG builds: LC_ATTN_BWD_FORM=<form>, LC_ATTN_BWD_SPLIT=1 (A/Bs)
+  const char* f = lc_diag_env("LC_ATTN_BWD_FORM");
+  if (f) return atoi(f);
+  const char* e = lc_diag_env("LC_ATTN_BWD_SPLIT");
+  return e && atoi(e) ? (int)ATTN_BWD_SPLIT : 0;
+}();
 
 }  // namespace
 
@@ -1013,6 +1308,12 @@ int lc_attn_bwd_fp8(hipStream_t st, int n_seq, int L, int H, const void* qkv, lo
   LC_LAUNCH_RET();
 }
 
+int lc_attn_bwd_set_form(int form) {
+  if (form < 0 || form > ATTN_BWD_TWO_PHASE) return LC_EINVAL;
+  g_attn_bwd_form = form;
+  return LC_OK;
+}
+
 int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long ldq, const void* O,
                 const void* dO, long ldo, const float* lse, void* dqkv, long lddq, int causal) {
   LC_CHECK_ARG(n_seq > 0 && L > 0 && L <= 256 && H > 0 && ldq >= 3 * H * 64 && ldo >= H * 64);
@@ -1023,12 +1324,29 @@ int lc_attn_bwd(hipStream_t st, int n_seq, int L, int H, const void* qkv, long l
   dim3 grid(n_seq * H);
   const float scale = 0.125f;
   // fused single-pass kernel (dS^T parked in LDS, 1 workgroup per CU) up to 224 keys; the split
-  // key-major + query-major pair beyond that (LDS) or when LC_ATTN_BWD_SPLIT=1
-  static const int force_split = [] {
-    const char* e = lc_diag_env("LC_ATTN_BWD_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  const bool split = force_split != 0;
+  // key-major + query-major pair beyond that (LDS); lc_attn_bwd_set_form selects another form
+  const int form = g_attn_bwd_form ? g_attn_bwd_form : ATTN_BWD_FUSED;
+  const bool split = form == ATTN_BWD_SPLIT;
+  if (form == ATTN_BWD_TWO_PHASE && nqb <= 7) {
+    switch (nqb) {
+#define LC_AB2(Q)                                                                               \
+  case Q:                                                                                      \
+    if (causal)                                                                                \
+      hipLaunchKernelGGL((attn_bwd2_kernel<Q, true>), grid, dim3(64 * Q), 0, st, L, H, D,      \
+                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
+                         lse, (bf16_t*)dqkv, lddq, scale, g_att2_ko);                          \
+    else                                                                                       \
+      hipLaunchKernelGGL((attn_bwd2_kernel<Q, false>), grid, dim3(64 * Q), 0, st, L, H, D,     \
+                         (const bf16_t*)qkv, ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo,    \
+                         lse, (bf16_t*)dqkv, lddq, scale, g_att2_ko);                          \
+    break;
+      LC_AB2(1) LC_AB2(2) LC_AB2(3) LC_AB2(4) LC_AB2(5) LC_AB2(6) LC_AB2(7)
+#undef LC_AB2
+      default:
+        return LC_EINVAL;
+    }
+    LC_LAUNCH_RET();
+  }
   if (nqb == 8) {
     hipLaunchKernelGGL(attn_bwd_kv_kernel<8>, grid, dim3(512), 0, st, L, H, D, (const bf16_t*)qkv,
                        ldq, (const bf16_t*)O, (const bf16_t*)dO, ldo, lse, (bf16_t*)dqkv, lddq,

@@ -1559,6 +1559,8 @@ struct TnProb {
   int pw;             // W panel width of the launch (128 or 256)
   const float* div;   // optional device scalar every result is divided by (a power-of-two
                       // gradient scale: exact), or nullptr
+  int w16;            // W holds IEEE halves (the half residual gradient): its fragments are
+                      // rounded to bf16 as read (h2s8: the values of ln_bwd's bf16 copy)
 };
 LC_DEV float tn_unscale(const TnProb& p, float v) { return p.div ? v / *p.div : v; }
 
@@ -1682,6 +1684,12 @@ gemm_tn_wide_kernel(TnProb p0, TnProb p1) {
         fsk[ks][j] = tr_frag_asm<128>(ss, row, wsv * 32 + j * 16 + (t & 3) * 4);
     }
     lds_wait0();
+    if (p.w16) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TI; ++i) fwk[ks][i] = h2s8(fwk[ks][i]);
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = ks * 32 + g * 8;
@@ -2338,7 +2346,7 @@ int lc_adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ld
 static int adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, long ldg,
                          const void* h, const void* z, long ldz, const void* dpre, float scale,
                          float* dWu, float* dbu, float* dWd, float* dbd, void* ws, long ws_bytes,
-                         const float* div) {
+                         const float* div, int g16 = 0) {
   LC_CHECK_ARG(M > 0 && D > 0 && D % 64 == 0 && ldg % 8 == 0 && ldz % 8 == 0 && ldg >= D &&
                ldz >= D);
   LC_CHECK_ARG(dWu != nullptr && dWd != nullptr);
@@ -2346,6 +2354,7 @@ static int adapter_wgrad(hipStream_t stream, int M, int D, const void* gout, lon
   up.div = down.div = div;
   // dWu[D][64] += scale * gout^T h ; dbu += scale * colsum(gout)
   up.W = static_cast<const bf16_t*>(gout);
+  up.w16 = g16;
   up.ldw = ldg;
   up.S = static_cast<const bf16_t*>(h);
   up.lds = 64;
@@ -2419,6 +2428,16 @@ int lc_adapter_wgrad_ws_unscaled(hipStream_t stream, int M, int D, const void* g
   LC_CHECK_ARG(gscale != nullptr);
   return adapter_wgrad(stream, M, D, gout, ldg, h, z, ldz, dpre, scale, dWu, dbu, dWd, dbd, ws,
                        ws_bytes, gscale);
+}
+
+// gout IEEE half (the image tower's half residual gradient, carrying the scale gscale)
+int lc_adapter_wgrad_ws_unscaled_g16(hipStream_t stream, int M, int D, const void* gout, long ldg,
+                                     const void* h, const void* z, long ldz, const void* dpre,
+                                     float scale, float* dWu, float* dbu, float* dWd, float* dbd,
+                                     void* ws, long ws_bytes, const float* gscale) {
+  LC_CHECK_ARG(gscale != nullptr);
+  return adapter_wgrad(stream, M, D, gout, ldg, h, z, ldz, dpre, scale, dWu, dbu, dWd, dbd, ws,
+                       ws_bytes, gscale, 1);
 }
 #endif
 

@@ -267,6 +267,35 @@ LC_DEV __amdgpu_buffer_rsrc_t lc_rsrc(const void* p, long bytes) {
 typedef unsigned int lc_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int lc_u32x2 __attribute__((ext_vector_type(2)));
 
+// A half residual gradient read as a 16-bit MFMA operand (the image tower, bf16 build): 8 IEEE
+// halves -> bf16 (round to nearest even), the values ln_bwd's bf16 copy of the same gradient
+// held (norm.hip ln_bwd_kernel rounds to half, then to bf16), so consumers reading the half
+// gradient directly reproduce the copy's results bit for bit. Identity in the LC_F16 build.
+LC_DEV bf16x8 h2s8(bf16x8 v) {
+#ifdef LC_F16
+  return v;
+#else
+  // (written out per dword: the same conversion as a loop over u[k] / o[k] compiled to dword 0
+  // converted and splatted into all four)
+  const lc_u32x4 u = __builtin_bit_cast(lc_u32x4, v);
+  const lc_f32x2 f0 = __builtin_convertvector(__builtin_bit_cast(lc_h16x2, (uint32_t)u.x), lc_f32x2);
+  const lc_f32x2 f1 = __builtin_convertvector(__builtin_bit_cast(lc_h16x2, (uint32_t)u.y), lc_f32x2);
+  const lc_f32x2 f2 = __builtin_convertvector(__builtin_bit_cast(lc_h16x2, (uint32_t)u.z), lc_f32x2);
+  const lc_f32x2 f3 = __builtin_convertvector(__builtin_bit_cast(lc_h16x2, (uint32_t)u.w), lc_f32x2);
+  return __builtin_bit_cast(bf16x8, (lc_u32x4{pack2bf(f0.x, f0.y), pack2bf(f1.x, f1.y),
+                                              pack2bf(f2.x, f2.y), pack2bf(f3.x, f3.y)}));
+#endif
+}
+// one half of a packed pair as the f32 value of its bf16 rounding (h2s8's scalar form)
+LC_DEV float h2s_f(uint32_t word, int hi) {
+  const float f = h2f((uint16_t)(hi ? word >> 16 : word & 0xffff));
+#ifdef LC_F16
+  return f;
+#else
+  return bf2f(f2bf(f));
+#endif
+}
+
 LC_DEV uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
 }

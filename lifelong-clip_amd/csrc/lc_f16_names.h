@@ -6,6 +6,7 @@
 #define lc_attn_fwd lc_attn_fwd_f16
 #define lc_attn_bwd_fp8 lc_attn_bwd_fp8_f16
 #define lc_attn_bwd lc_attn_bwd_f16
+#define lc_attn_bwd_set_form lc_attn_bwd_set_form_f16
 #define lc_gemm_nt_ex lc_gemm_nt_ex_f16
 #define lc_gemm_nt lc_gemm_nt_f16
 #define lc_gemm_nt_ws lc_gemm_nt_ws_f16

@@ -245,6 +245,9 @@ constexpr int AD_H = 64;  // adapter.py:38 hard-codes the down width (Q7)
 // from HBM once for both products (the two-GEMM form reads it twice and round-trips dpre).
 // Arithmetic is the GEMM epilogues' (EPI_AD_MASK, EPI_AD_ADD) with the same MFMA operand order
 // and k order, so the results are bit-identical to that path.
+// GH: g is the half residual gradient (IEEE half, the image tower's backward): its fragments and
+// values are rounded to bf16 as read (h2s8), the values of the bf16 copy the LayerNorm backward
+// would otherwise write for this kernel (the same results, 77 MB less written per layer).
 //   phase 1: dpre^T[j][m]: wave w owns the 16x16 tile j = 16 (w & 3) .., m = 16 (w >> 2) ..
 //   phase 2: dz^T[n][m] (K = 64): wave w owns n-tiles w ND/2 .. +ND/2-1 for both row tiles;
 //            dz is written over g in the LDS image and stored as whole rows
@@ -284,7 +287,7 @@ LC_DEV void wait_vm_dyn(int n) {
   }
 }
 
-template <int ND, bool DZ>
+template <int ND, bool DZ, bool GH = false>
 __global__ void __launch_bounds__(64 * AD_NW, 1)
 adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
                          const bf16_t* __restrict__ Hs, const bf16_t* __restrict__ WuT,
@@ -420,6 +423,10 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (GH) {
+#pragma unroll
+          for (int e = 0; e < GK; ++e) fb[grp & 1][e] = h2s8(fb[grp & 1][e]);
+        }
 #pragma unroll
         for (int e = 0; e < GK; ++e) a1 = mfma16(wu[grp * GK + e], fb[grp & 1][e], a1);
       }
@@ -481,7 +488,9 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
             float o[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              o[r] = bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff)) + (a2[j][r] * 1.0f + 0.0f);
+              o[r] = (GH ? h2s_f(gg[r >> 1], r & 1)
+                         : bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff))) +
+                     (a2[j][r] * 1.0f + 0.0f);
             const uint2 ob = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
             asm volatile("ds_write_b64 %0, %1"
                          :: "v"(xrow + ad_swz(tq, nn >> 3) * 16 + (nn & 7) * 2), "v"(ob) : "memory");
@@ -1471,6 +1480,40 @@ int lc_adapter_bwd_set_form(int fused) {
 
 //   dpre = (h > 0) ? scale * (gout Wu) / keep : 0    [M,64]  N = 64, K = D   (B = Wu^T)
 //   dz   = gout + dpre Wd                            [M,D]   N = D,  K = 64  (B = Wd^T)
+#ifndef LC_F16
+// gout IEEE half (the image tower's half residual gradient), everything else bf16: the
+// row-block kernel reading gout directly (any M; dz may be NULL: dpre only)
+int lc_adapter_bwd_g16(hipStream_t st, int M, int D, const void* gout, long ldg, const void* h,
+                       const void* WuT, const void* WdT, float scale, float keep, void* dpre,
+                       void* dz, long ldz) {
+  LC_CHECK_ARG(M > 0 && (D == 768 || D == 512) && ldg % 8 == 0 && ldz % 8 == 0);
+  LC_CHECK_ARG(keep > 0.f && keep <= 1.f);
+  LC_CHECK_ARG(((uintptr_t)gout & 15) == 0 && ((uintptr_t)h & 15) == 0 &&
+               ((uintptr_t)WuT & 15) == 0 && ((uintptr_t)WdT & 15) == 0 &&
+               (dz == nullptr || ((uintptr_t)dz & 15) == 0));
+  const int nb = (M + AD_R - 1) / AD_R;
+  const dim3 grid(nb < ad_cu_count() ? nb : ad_cu_count()), block(64 * AD_NW);
+  auto G = static_cast<const bf16_t*>(gout);
+  auto H = static_cast<const bf16_t*>(h);
+  auto U = static_cast<const bf16_t*>(WuT);
+  auto Wd = static_cast<const bf16_t*>(WdT);
+  auto P = static_cast<bf16_t*>(dpre);
+  auto Z = static_cast<bf16_t*>(dz);
+#define LC_ADB(ND, DZ)                                                                            \
+  hipLaunchKernelGGL((adapter_bwd_fused_kernel<ND, DZ, true>), grid, block, 0, st, M, G, ldg, H,  \
+                     U, Wd, scale, keep, P, Z, ldz)
+  if (D == 768) {
+    if (dz) LC_ADB(12, true);
+    else LC_ADB(12, false);
+  } else {
+    if (dz) LC_ADB(8, true);
+    else LC_ADB(8, false);
+  }
+#undef LC_ADB
+  LC_LAUNCH_RET();
+}
+#endif
+
 int lc_adapter_bwd(hipStream_t st, int M, int D, const void* gout, long ldg, const void* h,
                    const void* WuT, const void* WdT, float scale, float keep, void* dpre,
                    void* dz, long ldz) {

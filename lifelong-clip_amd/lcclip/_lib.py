@@ -29,6 +29,7 @@ SIGNATURES = {
     "lc_gemm_set_streamk": [c_int],
     "lc_gemm_set_debug": [P],
     "lc_adapter_bwd_set_form": [c_int],
+    "lc_attn_bwd_set_form": [c_int],
     "lc_gemm_tn": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float],
     "lc_gemm_tn_ws": [P, c_int, c_int, c_int, P, c_long, P, c_long, c_float, P, c_long, P, c_float,
                       P, c_long],
@@ -85,6 +86,7 @@ SIGNATURES = {
 # the IEEE-half (text tower) forms: same arguments (include/lc_clip.h, "IEEE-half storage")
 F16_ENTRY_POINTS = ("lc_gemm_nt", "lc_gemm_nt_ws", "lc_gemm_tn", "lc_gemm_tn_ws",
                     "lc_layernorm_fwd", "lc_layernorm_bwd", "lc_attn_fwd", "lc_attn_bwd",
+                    "lc_attn_bwd_set_form",
                     "lc_cast_bf16", "lc_merge_weight", "lc_cast_weights_bf16",
                     "lc_merge_weights_bf16", "lc_lora_grad", "lc_lora_grad_ws", "lc_adapter_fwd",
                     "lc_adapter_ln_fwd", "lc_adapter_bwd", "lc_adapter_wgrad",
@@ -96,6 +98,8 @@ SIGNATURES.update({n + "_x16": SIGNATURES[n] for n in (
     "lc_layernorm_fwd_fp8", "lc_layernorm_bwd_fp8")})
 SIGNATURES["lc_layernorm_bwd_g16"] = SIGNATURES["lc_layernorm_bwd"]
 SIGNATURES["lc_adapter_wgrad_ws_unscaled"] = SIGNATURES["lc_adapter_wgrad_ws"] + [P]
+SIGNATURES["lc_adapter_wgrad_ws_unscaled_g16"] = SIGNATURES["lc_adapter_wgrad_ws_unscaled"]
+SIGNATURES["lc_adapter_bwd_g16"] = SIGNATURES["lc_adapter_bwd"]
 SIGNATURES["lc_lora_grad_ws_unscaled"] = SIGNATURES["lc_lora_grad_ws"] + [P]
 
 _lib = None

@@ -42,7 +42,12 @@ _seed_counter = itertools.count(1)
 
 
 def _empty(shape, dtype, dev):
-    return torch.empty(shape, dtype=dtype, device=dev)
+    """(dtype None: a buffer that is not kept -> None)"""
+    return None if dtype is None else torch.empty(shape, dtype=dtype, device=dev)
+
+
+def _rows(t, n):
+    return None if t is None else t[:n]
 
 
 def _key(*tensors):
@@ -473,13 +478,20 @@ class BlockStack:
 
         dx float16 (the half residual stream's gradient, the fused adapter tower): every residual
         gradient is stored in half, carrying the power-of-two scale `gscale` (device f32 [1],
-        set by the caller: ops.grad_pow2_normalize) that the weight gradients divide out."""
+        set by the caller: ops.grad_pow2_normalize) that the weight gradients divide out. The
+        adapter tower then keeps no bf16 copies (dxb may be None): its adapter backward and
+        weight-gradient launches read the half gradient directly (ops.adapter_bwd / _wgrad
+        _g16 forms, bit-identical to reading the copy)."""
         M, D = dx.shape
         gdt = dx.dtype
         if gdt != F32 and (gscale is None or prompt_grads is not None
                            or any(s.get("P", 0) or "R" in s for s in saved)):
             raise ValueError("a half residual gradient needs its gscale and no prompt rows")
         self._gscale = gscale
+        # the half gradient's consumers read it directly: no bf16 copies (LayerNorm backward
+        # writes the half gradient only)
+        nocopy = gdt != F32 and self.half_grad_direct()
+        cdt = None if nocopy else self.dt  # the copies' type (None: not kept)
         main = torch.cuda.current_stream(dx.device)
         self._gs = grad_stream
         ev = None
@@ -496,12 +508,13 @@ class BlockStack:
         dqkv = _empty((Mmax, 3 * D), self.dt, dev)
         dz = _empty((Mmax, D), self.dt, dev) if self.variant == "adapter" else None
         dx_mid = _empty((Mmax, D), gdt, dev)
-        dx_midb = _empty((Mmax, D), self.dt, dev)
+        dx_midb = _empty((Mmax, D), cdt, dev)
         # output-gradient buffers: the incoming pair and one more (ping-pong); prompt layers
         # expand the current gradient into a free pair and compact their output back
-        pairs = [(dx, dxb), (_empty((Mmax, D), gdt, dev), _empty((Mmax, D), self.dt, dev))]
+        pairs = [(dx, None if nocopy else dxb),
+                 (_empty((Mmax, D), gdt, dev), _empty((Mmax, D), cdt, dev))]
         if keep_input:
-            pairs.append((_empty((Mmax, D), gdt, dev), _empty((Mmax, D), self.dt, dev)))
+            pairs.append((_empty((Mmax, D), gdt, dev), _empty((Mmax, D), cdt, dev)))
         cur = 0
         # fp8 (no adapter: the block output gradient feeds c_proj dX directly): ln_1's backward
         # also writes its result as the fp8 operand of the next (lower) block's c_proj dX GEMM
@@ -526,13 +539,14 @@ class BlockStack:
                     v[:, :L] = src[:M].view(n_seq, L, D)
                     v[:, L:] = 0
                 cur = e
-            gx, gxb = pairs[cur][0][:Mx], pairs[cur][1][:Mx]
+            gx, gxb = _rows(pairs[cur][0], Mx), _rows(pairs[cur][1], Mx)
             out = next(i for i in range(len(pairs)) if i != cur and (
                 i != 0 or (not keep_input and (P == 0 or pairs[0][0].shape[0] >= Mx))))
-            ox, oxb = pairs[out][0][:Mx], pairs[out][1][:Mx]
+            ox, oxb = _rows(pairs[out][0], Mx), _rows(pairs[out][1], Mx)
             # ---- MLP sub-block: x_out = x_mid + [A](c_proj(gelu(c_fc(ln_2(x_mid)))))
             if self.variant == "adapter":
-                dY = self._adapter_bwd(blk, st, gxb, s["hd2"], s["z2"], s["keep"], dz[:Mx], grads)
+                dY = self._adapter_bwd(blk, st, gx if nocopy else gxb, s["hd2"], s["z2"],
+                                       s["keep"], dz[:Mx], grads)
             else:
                 dY = gxb
             if q_da is not None:
@@ -545,12 +559,13 @@ class BlockStack:
                 self._gemm(st, "wprT", dY, EPI_MUL, da[:Mx], aux=s["gd"])
                 self._gemm(st, "wfcT", da[:Mx], EPI_BF16, dh[:Mx])
             ops.layernorm_bwd(dh[:Mx], s["x_mid"], s["mean2"], s["rstd2"], blk.ln_2.weight,
-                              dx_mid[:Mx], dx_midb[:Mx], dres=gx)
+                              dx_mid[:Mx], _rows(dx_midb, Mx), dres=gx)
             # ---- attention sub-block: x_mid = x_in + [A](out_proj(attn(ln_1(x_in))))
             first = li == 0 and not need_dx
             if self.variant == "adapter":
-                dY = self._adapter_bwd(blk, st, dx_midb[:Mx], s["hd1"], s["z1"], s["keep"],
-                                       None if first else dz[:Mx], grads)
+                dY = self._adapter_bwd(blk, st, dx_mid[:Mx] if nocopy else dx_midb[:Mx],
+                                       s["hd1"], s["z1"], s["keep"], None if first else dz[:Mx],
+                                       grads)
             else:
                 dY = dx_midb[:Mx]
             if first and self.variant != "lora":
@@ -617,7 +632,7 @@ class BlockStack:
         self._gscale = None
         if not need_dx:
             return None, None
-        return pairs[cur][0][:M], pairs[cur][1][:M]
+        return pairs[cur][0][:M], _rows(pairs[cur][1], M)
 
     @staticmethod
     def _layer_done(li, grad_stream, on_layer):
@@ -665,6 +680,15 @@ class BlockStack:
                               self._grad(grads, ad.down_proj.bias),
                               gscale=getattr(self, "_gscale", None))
         return dz
+
+    # LCCLIP_HALF_GRAD_DIRECT=0: the adapter tower's half residual gradient with bf16 copies for
+    # its adapter backward launches, as before lc_adapter_*_g16 (A/B experiments)
+    HALF_GRAD_DIRECT = os.environ.get("LCCLIP_HALF_GRAD_DIRECT", "0") != "0"
+
+    def half_grad_direct(self):
+        """A half residual gradient's consumers read it directly (no bf16 copies): the adapter
+        tower (its adapter backward launches have _g16 forms)."""
+        return self.variant == "adapter" and self.HALF_GRAD_DIRECT
 
     # LCCLIP_PROMPT_KEEP=0: compact and re-expand between prompt layers of one prompt count
     # (A/B experiments)
@@ -1046,6 +1070,8 @@ class ImageTower:
         ops.gemm_nt(dfb, self.proj, EPI_F32, dln)
         dx, dxb = self._grad_in.get(n * L, D, dev, ctx["cls_idx"], key=(n, L),
                                     dt=dt, gdt=F16 if half else F32)
+        if half and self.stack.half_grad_direct():
+            dxb = None  # the adapter backward reads the half gradient itself (no bf16 copy)
         ops.layernorm_bwd(dln, ctx["x"], ctx["mean"], ctx["rstd"], v.ln_post.weight, dx, dxb,
                           row_idx=ctx["cls_idx"])
         # the input (patch embedding) is frozen; prompts appended at layer 0 need its backward

@@ -501,11 +501,25 @@ def adapter_ln_fwd(z, Wd, bd, Wu, bu, scale, keep, seed, resid, xout, h, gamma, 
          y.stride(0), ptr(mean), ptr(rstd))
 
 
+def _g16(name, gout, *ts):
+    """lc_adapter_*_g16 for a float16 gout beside bf16 partners (the image tower's half
+    residual gradient, read directly: include/lc_clip.h), else the storage-type entry point."""
+    if gout.dtype == F16 and any(t is not None and t.dtype == BF16 for t in ts):
+        if any(t is not None and t.dtype == F16 for t in ts):
+            raise TypeError(f"{name}: a float16 gout takes bf16 partners")
+        if gout.stride(-1) != 1 or gout.stride(0) % 8 or gout.data_ptr() % 16:
+            raise ValueError(f"{name}: half gout must be row-major, 16-B aligned, row stride % 8")
+        return name + "_g16"
+    return _sym16(name, gout, *ts)
+
+
 def adapter_bwd(gout, h, WuT, WdT, scale, keep, dpre, dz):
+    """dpre, dz (adapter.py:59-72 autograd). gout float16 with bf16 partners: the half residual
+    gradient read directly (lc_adapter_bwd_g16, the same results as its bf16 copy)."""
     M, D = gout.shape
-    call(_sym16("lc_adapter_bwd", gout, h, WuT, WdT, dpre, dz), stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(WuT),
-         ptr(WdT), float(scale), float(keep), ptr(dpre), ptr(dz),
-         dz.stride(0) if dz is not None else D)
+    call(_g16("lc_adapter_bwd", gout, h, WuT, WdT, dpre, dz), stream_of(gout), M, D, ptr(gout),
+         gout.stride(0), ptr(h), ptr(WuT), ptr(WdT), float(scale), float(keep), ptr(dpre),
+         ptr(dz), dz.stride(0) if dz is not None else D)
 
 
 def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd, gscale=None):
@@ -527,12 +541,17 @@ def adapter_wgrad(gout, h, z, dpre, scale, dWu, dbu, dWd, dbd, gscale=None):
     # ticket region; the stream orders every user of that buffer)
     ws = splitk_workspace(torch.cuda.current_stream(gout.device))
     if gscale is not None:
-        if gout.dtype != BF16 or gscale.dtype != F32 or gscale.numel() != 1:
-            raise TypeError("adapter_wgrad: gscale takes bf16 operands and an f32 device scalar")
-        call("lc_adapter_wgrad_ws_unscaled", stream_of(gout), M, D, ptr(gout), gout.stride(0),
+        # gout bf16, or float16 (the half residual gradient read directly: the _g16 form)
+        name = _g16("lc_adapter_wgrad_ws_unscaled", gout, h, z, dpre)
+        if (h.dtype != BF16 or z.dtype != BF16 or dpre.dtype != BF16 or gscale.dtype != F32
+                or gscale.numel() != 1):
+            raise TypeError("adapter_wgrad: gscale takes bf16 partners and an f32 device scalar")
+        call(name, stream_of(gout), M, D, ptr(gout), gout.stride(0),
              ptr(h), ptr(z), z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd),
              ptr(dbd), ptr(ws), ws.numel(), ptr(gscale))
         return
+    if gout.dtype != h.dtype:
+        raise TypeError("adapter_wgrad: a float16 gout beside bf16 operands needs its gscale")
     call(_sym16("lc_adapter_wgrad_ws", gout, h, z, dpre), stream_of(gout), M, D, ptr(gout), gout.stride(0), ptr(h), ptr(z),
          z.stride(0), ptr(dpre), float(scale), ptr(dWu), ptr(dbu), ptr(dWd), ptr(dbd), ptr(ws),
          ws.numel())

@@ -134,7 +134,8 @@ def test_peft_walkers_do_not_spill(peft_asm):
     loads and stores to that count. Its reloads also wait vmcnt(0) and drain the DMAs in flight.
     (r4: a variant with contiguous per-walker row shares spilled 4 B per lane in
     adapter_ln_fwd<768> — hoisted per-lane DMA addresses — until its DMA lambdas recomputed their
-    lane terms.) Every instantiation keeps ScratchSize 0."""
+    lane terms.) Every instantiation keeps ScratchSize 0: adapter_ln_fwd (4), adapter_bwd_fused
+    <12|8, dz> (2) and its half-gradient forms <12|8, dz|dpre only, g16> (4)."""
     found = 0
     for m in re.finditer(r"^(_ZN12_GLOBAL__N_1\d+(adapter_ln_fwd_kernel|adapter_bwd_fused_kernel)"
                          r"I\w+?EE\w*):", peft_asm, re.M):
@@ -142,4 +143,4 @@ def test_peft_walkers_do_not_spill(peft_asm):
         scratch = re.search(r"; ScratchSize: (\d+)", peft_asm[end:end + 4000])
         assert scratch and int(scratch.group(1)) == 0, f"{m.group(1)} spills: {scratch.group(0)}"
         found += 1
-    assert found == 6, found
+    assert found == 10, found

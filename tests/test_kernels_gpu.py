@@ -345,6 +345,47 @@ def test_attention_fwd_bwd(ops, dev, n, L, H, causal):
     assert rel(g[2], v.grad) < 2e-2
 
 
+@pytest.mark.parametrize("n,L,H,causal", [(3, 17, 2, False), (4, 77, 8, True), (2, 197, 12, False),
+                                          (5, 32, 1, True), (2, 200, 2, False), (3, 224, 2, False),
+                                          (2, 213, 3, True), (1, 193, 2, False), (2, 202, 2, False),
+                                          (1, 250, 2, False), (3, 100, 2, True)])
+def test_attention_bwd_forms(ops, dev, n, L, H, causal):
+    """Every lc_attn_bwd form (lc_attn_bwd_set_form: 1 fused dS^T park, 2 key-major + query-major
+    pair, 3 two-phase at two workgroups per CU) against the torch fp32 gradient of the attention
+    actually computed, and against each other: the same bf16 dS / P operands, so they differ only
+    where an f32 sum order flips a bf16 rounding (lora.py:1043-1068 autograd)."""
+    from lcclip import _lib
+    torch.manual_seed(5)
+    D = H * 64
+    lib = _lib.load()
+    qkv = (torch.randn(n * L, 3 * D, device=dev) * 1.5).to(BF)
+    O = torch.empty(n * L, D, device=dev, dtype=BF)
+    lse = torch.empty(n * H, L, device=dev)
+    ops.attn_fwd(qkv, O, lse, n, L, H, causal)
+    t = qkv.float().reshape(n, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = (x.clone().requires_grad_(True) for x in t)
+    dO = torch.randn(n * L, D, device=dev).to(BF)
+    ref_attention(q, k, v, causal).backward(dO.float().reshape(n, L, H, 64).permute(0, 2, 1, 3))
+    outs = {}
+    try:
+        for form in (1, 2, 3):
+            assert lib.lc_attn_bwd_set_form(form) == 0
+            dqkv = torch.full((n * L, 3 * D), float("nan"), device=dev, dtype=BF)
+            ops.attn_bwd(qkv, O, dO, lse, dqkv, n, L, H, causal)
+            torch.cuda.synchronize()
+            g = dqkv.float().reshape(n, L, 3, H, 64).permute(2, 0, 3, 1, 4)
+            assert torch.isfinite(g).all(), form
+            for i, ref in enumerate((q.grad, k.grad, v.grad)):
+                assert rel(g[i], ref) < 2e-2, (form, i)
+            outs[form] = g
+    finally:
+        lib.lc_attn_bwd_set_form(0)
+    assert lib.lc_attn_bwd_set_form(4) != 0
+    for form in (2, 3):
+        for i in range(3):
+            assert rel(outs[form][i], outs[1][i]) < 4e-3, (form, i)
+
+
 # ------------------------------------------------------------------------------- train transform
 @pytest.mark.parametrize("params", [(0, 0, False), (8, 8, True), (3, 5, True), (4, 4, False)])
 def test_train_transform_vs_oracle(dev, params):
@@ -879,6 +920,10 @@ def test_layernorm_bwd_g16(ops, dev, D):
     ops.layernorm_bwd(dy, xh, mu, rs, gam, dx16, dxb16, dres=dres)
     assert torch.equal(dx16, dx32.to(H16))
     assert torch.equal(dxb16, dx16.float().to(BF))
+    # without the copy (the adapter tower): the same half result
+    dxn = torch.full((M, D), float("nan"), device=dev, dtype=H16)
+    ops.layernorm_bwd(dy, xh, mu, rs, gam, dxn, None, dres=dres)
+    assert torch.equal(dxn, dx16)
     # row-gathered, no dres (ln_post's backward into the CLS rows)
     idx = torch.arange(0, M, 197, device=dev, dtype=torch.int32)
     dl = torch.randn(idx.numel(), D, device=dev) * 10
@@ -914,6 +959,46 @@ def test_adapter_wgrad_unscaled(ops, dev):
         outs.append(bufs)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("D,M", [(768, 50432), (768, 3152), (512, 2013), (768, 394), (768, 31)])
+def test_adapter_g16_matches_bf16_copy(ops, dev, D, M):
+    """lc_adapter_bwd_g16 / lc_adapter_wgrad_ws_unscaled_g16 read the half residual gradient
+    itself and give, bit for bit, what lc_adapter_bwd / _wgrad_ws_unscaled give on the bf16 copy
+    lc_layernorm_bwd_g16 writes of it (bf16 of the half value): dpre, dz and the dpre-only call,
+    and all four weight / bias gradients. Includes gradients in half's subnormal range and row
+    counts below one walker block (adapter.py:59-72 autograd)."""
+    torch.manual_seed(D + M)
+    H16 = torch.float16
+    g32 = torch.randn(M, D, device=dev) * 2.0 ** torch.randint(-22, 4, (M, 1), device=dev)
+    g16 = g32.to(H16)
+    gb = g16.float().to(BF)  # the copy: norm.hip rounds the stored half value to bf16
+    h = torch.relu(torch.randn(M, 64, device=dev)).to(BF)
+    z = torch.randn(M, D, device=dev).to(BF)
+    Wu = (torch.randn(D, 64, device=dev) * 0.125).to(BF)
+    Wd = (torch.randn(64, D, device=dev) * D ** -0.5).to(BF)
+    WuT, WdT = Wu.t().contiguous(), Wd.t().contiguous()
+    gs = torch.full((1,), 2.0 ** 12, device=dev)
+    res = {}
+    for name, g in (("copy", gb), ("g16", g16)):
+        dpre = torch.full((M, 64), 7.0, device=dev, dtype=BF)
+        dz = torch.full((M, D), 7.0, device=dev, dtype=BF)
+        ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre, dz)
+        dpre1 = torch.full((M, 64), 7.0, device=dev, dtype=BF)
+        ops.adapter_bwd(g, h, WuT, WdT, 0.1, 0.9, dpre1, None)
+        bufs = [torch.zeros(D, 64, device=dev), torch.zeros(D, device=dev),
+                torch.zeros(64, D, device=dev), torch.zeros(64, device=dev)]
+        ops.adapter_wgrad(g, h, z, dpre, 0.1, *bufs, gscale=gs)
+        torch.cuda.synchronize()
+        res[name] = [dpre, dz, dpre1] + bufs
+    for a, b in zip(res["copy"], res["g16"]):
+        assert torch.equal(a, b)
+    # and against torch fp32 on the copy's values
+    dh = 0.1 * gb.float() @ Wu.float()
+    assert rel(res["g16"][0], torch.where(h.float() > 0, dh / 0.9, torch.zeros_like(dh))) < 4e-3
+    assert rel(res["g16"][3], 0.1 * gb.float().t() @ h.float() / 2.0 ** 12) < 1e-4
+    with pytest.raises(TypeError):  # a half gout beside half partners has no such form
+        ops.adapter_wgrad(g16, h.half(), z.half(), res["g16"][0].half(), 0.1, *bufs, gscale=gs)
 
 
 @pytest.mark.parametrize("K,N", [(768, 2304), (768, 768)])

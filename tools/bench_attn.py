@@ -1,7 +1,8 @@
 """Attention fwd/bwd microbenchmark at the ViT-B/16 B=256 image shape and the text shape (dev tool).
 
 Prints one line per kernel: average ms over REPS launches, achieved TFLOP/s (algorithmic, unpadded
-L: fwd 2 matmuls, bwd 5 matmuls of L x L x 64 per (sequence, head))."""
+L: fwd 2 matmuls, bwd 5 matmuls of L x L x 64 per (sequence, head)). FORMS=1,2,3 times each
+lc_attn_bwd_set_form form of the backward in turn (default: the automatic one)."""
 import os
 import sys
 
@@ -9,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "lifelong-clip_amd")]
 import torch  # noqa: E402
 
-from lcclip import ops  # noqa: E402
+from lcclip import _lib, ops  # noqa: E402
 
 REPS = int(os.environ.get("REPS", 20))
 dev = torch.device("cuda:0")
@@ -39,5 +40,9 @@ def run(name, n, L, H, causal):
               flush=True)
 
 
-run("image", int(os.environ.get("B", 256)), 197, 12, False)
-run("text", int(os.environ.get("C", 100)), 77, 8, True)
+for form in [int(f) for f in os.environ.get("FORMS", "0").split(",")]:
+    if _lib.load().lc_attn_bwd_set_form(form) != 0:
+        raise SystemExit(f"lc_attn_bwd_set_form({form}) rejected")
+    print(f"-- backward form {form}", flush=True)
+    run("image", int(os.environ.get("B", 256)), 197, 12, False)
+    run("text", int(os.environ.get("C", 100)), 77, 8, True)

@@ -2,7 +2,7 @@
 # PMC passes over tools/bench_attn.py (run on the GPU box, from the repo root). FETCH_SIZE (3 TCC
 # slots) and WRITE_SIZE (2) never share a pass (4 TCC slots per pass).
 set -e
-export TMPDIR=/tmp REPS=3
+export TMPDIR=/tmp REPS=3 FORMS=${FORMS:-0}
 P=gpurun_out/pmc_attn
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS --output-format csv -d ${P}_a -o p -- python tools/bench_attn.py > /dev/null 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE FETCH_SIZE --output-format csv -d ${P}_b -o p -- python tools/bench_attn.py > /dev/null 2>&1
