@@ -205,12 +205,14 @@ int lc_adapter_wgrad_ws_unscaled(hipStream_t stream, int M, int D, const void* g
                                  float scale, float* dWu, float* dbu, float* dWd, float* dbd,
                                  void* ws, long ws_bytes, const float* gscale);
 /* The two adapter backward launches reading the half residual gradient itself: gout IEEE half
- * [M, ldg] (16-B aligned), every other 16-bit operand bf16. Each gout value enters as its bf16
- * rounding, the value lc_layernorm_bwd_g16's dx_bf16 copy holds, so the results equal
- * lc_adapter_bwd / lc_adapter_wgrad_ws_unscaled on that copy bit for bit, without it being
- * written (77 MB per LayerNorm backward at ViT-B/16 B = 256). lc_adapter_bwd_g16: D = 512 or
- * 768, any M, dz may be NULL (dpre only). Replaces: adapter.py:59-72 autograd, as lc_adapter_bwd
- * and lc_adapter_wgrad. */
+ * [M, ldg] (16-B aligned), every other 16-bit operand bf16, so lc_layernorm_bwd_g16 writes no
+ * bf16 copy (77 MB per LayerNorm backward at ViT-B/16 B = 256).
+ * lc_adapter_bwd_g16: dpre = mask(scale * gout Wu) / keep on the f16 MFMA (Wu cast to half, the
+ * reference's fp16 autocast product), dz = gout + dpre Wd with the exact half gout; D = 512 or
+ * 768, any M, dz may be NULL (dpre only).
+ * lc_adapter_wgrad_ws_unscaled_g16: each gout value enters as its bf16 rounding (the value the
+ * copy held): the results equal lc_adapter_wgrad_ws_unscaled on the copy bit for bit.
+ * Replaces: adapter.py:59-72 autograd, as lc_adapter_bwd and lc_adapter_wgrad. */
 int lc_adapter_bwd_g16(hipStream_t stream, int M, int D, const void* gout, long ldg, const void* h,
                        const void* WuT, const void* WdT, float scale, float keep, void* dpre,
                        void* dz, long ldz);

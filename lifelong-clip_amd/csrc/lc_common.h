@@ -286,14 +286,20 @@ LC_DEV bf16x8 h2s8(bf16x8 v) {
                                               pack2bf(f2.x, f2.y), pack2bf(f3.x, f3.y)}));
 #endif
 }
-// one half of a packed pair as the f32 value of its bf16 rounding (h2s8's scalar form)
-LC_DEV float h2s_f(uint32_t word, int hi) {
-  const float f = h2f((uint16_t)(hi ? word >> 16 : word & 0xffff));
-#ifdef LC_F16
-  return f;
-#else
-  return bf2f(f2bf(f));
-#endif
+// 8 bf16 -> IEEE half (round to nearest even; |x| < 2^-24 flushes to zero, as the reference's
+// fp16 autocast cast of the same weight, methods/adapter_clip.py:87)
+LC_DEV bf16x8 b2h8(bf16x8 v) {
+  const lc_u32x4 u = __builtin_bit_cast(lc_u32x4, v);
+  auto cv = [](uint32_t w) {
+    return pack2h(__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u));
+  };
+  return __builtin_bit_cast(bf16x8, (lc_u32x4{cv(u.x), cv(u.y), cv(u.z), cv(u.w)}));
+}
+// v_mfma_f32_16x16x32_f16 on 8-half fragments (either storage build)
+LC_DEV f32x4 mfma16_h(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b),
+                                                c, 0, 0, 0);
 }
 
 LC_DEV uint32_t lds_addr(const void* p) {

@@ -245,9 +245,11 @@ constexpr int AD_H = 64;  // adapter.py:38 hard-codes the down width (Q7)
 // from HBM once for both products (the two-GEMM form reads it twice and round-trips dpre).
 // Arithmetic is the GEMM epilogues' (EPI_AD_MASK, EPI_AD_ADD) with the same MFMA operand order
 // and k order, so the results are bit-identical to that path.
-// GH: g is the half residual gradient (IEEE half, the image tower's backward): its fragments and
-// values are rounded to bf16 as read (h2s8), the values of the bf16 copy the LayerNorm backward
-// would otherwise write for this kernel (the same results, 77 MB less written per layer).
+// GH: g is the half residual gradient (IEEE half, the image tower's backward), read as written
+// (no bf16 copy from the LayerNorm backward: 77 MB less written per layer): phase 1 runs on the
+// f16 MFMA with Wu^T's fragments cast to half once per launch (the reference's fp16 autocast
+// product, methods/adapter_clip.py:87; rounding g to bf16 per fragment instead cost the walker
+// 42 -> 51 us), and phase 2 adds the exact half g.
 //   phase 1: dpre^T[j][m]: wave w owns the 16x16 tile j = 16 (w & 3) .., m = 16 (w >> 2) ..
 //   phase 2: dz^T[n][m] (K = 64): wave w owns n-tiles w ND/2 .. +ND/2-1 for both row tiles;
 //            dz is written over g in the LDS image and stored as whole rows
@@ -341,6 +343,10 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
 #pragma unroll
     for (int ks = 0; ks < 2 * ND; ++ks)
       wu[ks] = *reinterpret_cast<const bf16x8*>(smem + (16 * nt1 + t) * (D * 2) + (ks * 4 + g) * 16);
+    if constexpr (GH) {
+#pragma unroll
+      for (int ks = 0; ks < 2 * ND; ++ks) wu[ks] = b2h8(wu[ks]);
+    }
     __syncthreads();
   }
   if constexpr (DZ) {
@@ -423,12 +429,10 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (GH) {
 #pragma unroll
-          for (int e = 0; e < GK; ++e) fb[grp & 1][e] = h2s8(fb[grp & 1][e]);
-        }
-#pragma unroll
-        for (int e = 0; e < GK; ++e) a1 = mfma16(wu[grp * GK + e], fb[grp & 1][e], a1);
+        for (int e = 0; e < GK; ++e)
+          a1 = GH ? mfma16_h(wu[grp * GK + e], fb[grp & 1][e], a1)
+                  : mfma16(wu[grp * GK + e], fb[grp & 1][e], a1);
       }
       // EPI_AD_MASK: v = acc * scale (+ no bias); (h > 0) ? v / keep : 0
       const int col = 16 * nt1 + 4 * g;
@@ -488,7 +492,7 @@ adapter_bwd_fused_kernel(int M, const bf16_t* __restrict__ G, long ldg,
             float o[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              o[r] = (GH ? h2s_f(gg[r >> 1], r & 1)
+              o[r] = (GH ? h2f((uint16_t)((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff)))
                          : bf2f((r & 1) ? (gg[r >> 1] >> 16) : (gg[r >> 1] & 0xffff))) +
                      (a2[j][r] * 1.0f + 0.0f);
             const uint2 ob = uint2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};

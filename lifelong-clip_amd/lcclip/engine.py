@@ -683,7 +683,7 @@ class BlockStack:
 
     # LCCLIP_HALF_GRAD_DIRECT=0: the adapter tower's half residual gradient with bf16 copies for
     # its adapter backward launches, as before lc_adapter_*_g16 (A/B experiments)
-    HALF_GRAD_DIRECT = os.environ.get("LCCLIP_HALF_GRAD_DIRECT", "0") != "0"
+    HALF_GRAD_DIRECT = os.environ.get("LCCLIP_HALF_GRAD_DIRECT", "1") != "0"
 
     def half_grad_direct(self):
         """A half residual gradient's consumers read it directly (no bf16 copies): the adapter
