@@ -69,6 +69,22 @@ LC_DEV uint4 ld16_or_zero(const bf16_t* p, bool ok) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Raw-buffer descriptor over `rows` rows of `row_bytes` from row row0 of p (wave-uniform): loads
+// past the range read zero and stores there are dropped by the range check, so no branch
+// surrounds a memory op and hipcc counts vmcnt across them (a load under a branch is followed by
+// vmcnt(0): the loads issued before it stop being in flight together).
+LC_DEV __amdgpu_buffer_rsrc_t seq_rsrc(const void* p, long row0, long row_bytes, int rows) {
+  const uint64_t a = (uint64_t)(static_cast<const char*>(p) + row0 * row_bytes);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int nb = __builtin_amdgcn_readfirstlane((int)(rows * row_bytes));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+}
+LC_DEV uint4 seq_ld16(__amdgpu_buffer_rsrc_t r, int off) {  // nontemporal (read once)
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 // Lane offsets (bytes) into a swizzled 128-B-row image, valid for any row block that starts at a
 // multiple of 16 rows:
 //   row_off(t, g, s): A/B-operand read of row t (+block), k-chunk s*4+g  (16 B)
@@ -123,16 +139,18 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
   const long base = (long)n * L;
   const float c = scale * LOG2E;
 
-  // staging: every lane issues all its 16-B loads before its first LDS write
+  // staging: every lane issues all its 16-B loads (through the sequence's descriptor: rows >= L
+  // read zero) before its first LDS write
   constexpr int IT = LP * 8 / NTH;  // = 4
   const int ch = tid & 7;
+  const auto rq = seq_rsrc(qkv, base, ldq * 2, L);
   uint4 kv[IT], vv[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int r = (tid + i * NTH) >> 3;
-    const bf16_t* src = qkv + (base + r) * ldq + h * 64 + ch * 8;
-    kv[i] = ld16_or_zero(src + D, r < L);
-    vv[i] = ld16_or_zero(src + 2 * D, r < L);
+    const int off = r * (int)ldq * 2 + (h * 64 + ch * 8) * 2;
+    kv[i] = seq_ld16(rq, off + D * 2);
+    vv[i] = seq_ld16(rq, off + D * 4);
   }
   const int qb = 32 * w;
   bf16x8 qf[2][2];
@@ -141,7 +159,7 @@ attn_fwd_kernel(int L, int H, int D, const bf16_t* __restrict__ qkv, long ldq,
     const int q = qb + qt * 16 + t;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      uint4 u = ld16_or_zero(qkv + (base + q) * ldq + h * 64 + s * 32 + g * 8, q < L);
+      uint4 u = seq_ld16(rq, q * (int)ldq * 2 + (h * 64 + s * 32 + g * 8) * 2);
       qf[qt][s] = *reinterpret_cast<bf16x8*>(&u);
     }
   }
