@@ -360,6 +360,9 @@ def main():
     ap.add_argument("--streamk", type=int, default=None,
                     help="A/B knob: lc_gemm_set_streamk mode (0 off, 1 N=768 K>=2048, 2 N=768, "
                          "3 every ragged 256x256 launch; default: the library's)")
+    ap.add_argument("--attn-bwd-form", type=int, default=None,
+                    help="A/B knob: lc_attn_bwd_set_form (1 fused dS^T park, 2 split pair, "
+                         "3 two-phase at two workgroups per CU; default: the library's)")
     ap.add_argument("--resid32", action="store_true",
                     help="A/B knob: the image tower's residual stream in f32 instead of IEEE half")
     args = ap.parse_args()
@@ -390,6 +393,10 @@ def main():
         from lcclip import _lib
         if _lib.load().lc_gemm_set_streamk(args.streamk) != 0:
             raise SystemExit(f"--streamk {args.streamk} rejected")
+    if args.attn_bwd_form is not None:
+        from lcclip import _lib
+        if _lib.load().lc_attn_bwd_set_form(args.attn_bwd_form) != 0:
+            raise SystemExit(f"--attn-bwd-form {args.attn_bwd_form} rejected")
     if args.resid32:
         from lcclip.engine import ImageTower
         ImageTower.RESID16 = False
