@@ -50,3 +50,21 @@ for r in side:
     sagg[key][1] += r["e"] - r["s"]
 for k, (n, t) in sorted(sagg.items(), key=lambda kv: -kv[1][1])[:20]:
     print(f"  {n:3d} {t / 1e3:8.1f}  q{k[2]} grid {k[1]:>8} {k[0]}")
+
+
+def short(name):
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0][:48]
+
+
+print("main-stream gaps by (previous kernel -> next kernel): count, total us, avg us")
+gagg = collections.defaultdict(lambda: [0, 0])
+for j in range(len(main) - 1):
+    g = main[j + 1]["s"] - main[j]["e"]
+    key = (short(main[j]["Kernel_Name"]), short(main[j + 1]["Kernel_Name"]))
+    gagg[key][0] += 1
+    gagg[key][1] += max(g, 0)
+for k, (n, t) in sorted(gagg.items(), key=lambda kv: -kv[1][1])[:30]:
+    print(f"  {n:3d} {t / 1e3:8.1f} {t / n / 1e3:7.1f}  {k[0]} -> {k[1]}")
+hist = collections.Counter(min(int(max(g, 0) / 1e3 // 2) * 2, 40) for g, _, _ in gaps)
+print("gap histogram (us bucket: count):", dict(sorted(hist.items())))
