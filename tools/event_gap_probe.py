@@ -7,6 +7,7 @@ separated by a synchronize so the trace can tell them apart:
   side       k1, side.wait_stream(main) + a small kernel on the side stream, k2
   waitside   k1, main.wait_event(event recorded on an idle side stream), k2
 then (tools/trace_gaps_probe below) prints the average k1 -> k2 gap per form."""
+import os
 import sys
 import torch
 
@@ -19,7 +20,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "report":
         qs.setdefault(r["Queue_Id"], 0)
         qs[r["Queue_Id"]] += 1
     mq = max(qs, key=qs.get)
-    main = [r for r in rows if r["Queue_Id"] == mq]
+    main = [r for r in rows if r["Queue_Id"] == mq and "mul" not in r["Kernel_Name"].lower()]
     forms = ["plain", "record", "side", "waitside"]
     # the probe's main-stream kernels come in blocks of 200 (100 pairs) per form, after 20 warmup
     k = main[20:]
@@ -33,6 +34,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "report":
     raise SystemExit(0)
 
 dev = torch.device("cuda:0")
+busy = os.environ.get("PROBE_BUSY") == "1"  # a third stream kept busy meanwhile (the text tower)
 a = torch.zeros(16 << 20, device=dev)
 b = torch.zeros(16 << 20, device=dev)
 c = torch.zeros(1024, device=dev)
@@ -42,7 +44,13 @@ for _ in range(10):
     a.add_(1.0)
     b.add_(1.0)
 torch.cuda.synchronize()
+third = torch.cuda.Stream()
+big = torch.zeros(64 << 20, device=dev)
 for form in ("plain", "record", "side", "waitside"):
+    if busy:
+        with torch.cuda.stream(third):
+            for _ in range(60):
+                big.mul_(1.0)
     for _ in range(100):
         a.add_(1.0)
         if form == "record":
