@@ -363,6 +363,10 @@ def main():
     ap.add_argument("--attn-bwd-form", type=int, default=None,
                     help="A/B knob: lc_attn_bwd_set_form (1 fused dS^T park, 2 split pair, "
                          "3 two-phase at two workgroups per CU; default: the library's)")
+    ap.add_argument("--peft-encoder", default=None, choices=["both", "image", "text", "none"],
+                    help="which towers carry the PEFT residuals (AdapterCLIP peft_encoder; default "
+                         "both, config 2's; 'image' freezes the text tower, whose features are "
+                         "then cached across steps: a measurement of the text tower's cost)")
     ap.add_argument("--resid32", action="store_true",
                     help="A/B knob: the image tower's residual stream in f32 instead of IEEE half")
     args = ap.parse_args()
@@ -402,6 +406,8 @@ def main():
         ImageTower.RESID16 = False
     torch.manual_seed(1234)  # identical random-init weights on every rank
     peft = "both" if args.method != "vanilla" else "none"
+    if args.peft_encoder is not None:
+        peft = args.peft_encoder
     model = AdapterCLIP("ViT-B/16", peft_method=args.method, peft_encoder=peft, device=dev,
                         text_precision=args.text_precision, image_precision=args.image_precision)
     trainer = OnlineTrainer(model, distributed=dp,
@@ -481,7 +487,8 @@ def main():
                         and trainer.img.stack.lora_half_grad_ok()))) else "f32",
             "data": "synthetic (random-init ViT-B/16 CLIP weights, U[0,1) images normalised with "
                     "CIFAR-100 stats, random prompt token ids)",
-            "config": {"workload": f"{args.method}_clip ViT-B/16 both towers, online_train step "
+            "config": {"workload": f"{args.method}_clip ViT-B/16 "
+                                   f"{'both towers' if peft == 'both' else 'peft_encoder=' + peft}, online_train step "
                                    f"(fwd + CE-on-probs + bwd + AdamW)",
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": 197,
                        "text_prompts": C, "parallelism": f"dp{world}",
