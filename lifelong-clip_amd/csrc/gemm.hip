@@ -2115,6 +2115,22 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     g_force_tile = e ? atoi(e) : 0;
   }
   int tile = g_force_tile;
+#ifndef LC_F16
+  // the QKV input-gradient GEMM of a 256-image step (plain: no epilogue, no bias) on hipBLASLt
+  // (blaslt.hip: 142 vs 160 us standalone, step +1.2 %); its workspace is the split-K scratch
+  // after the tickets. A forced tile (A/B tools) or LC_GEMM_BLASLT=0 (DIAG) keeps gemm8.
+  static const bool use_blaslt = [] {
+    const char* e = lc_diag_env("LC_GEMM_BLASLT");
+    return !(e && e[0] == '0');
+  }();
+  if (use_blaslt && tile == 0 && epi == EPI_BF16 && bias == nullptr && alpha == 1.0f &&
+      M >= 32768 && N == 768 && K == 2304 && ws != nullptr &&
+      ws_bytes >= LC_SPLITK_TICKET_BYTES + (8L << 20) &&
+      lc_blaslt_nt_bf16(stream, M, N, K, a, lda, b, ldb, out0, ldo0,
+                        static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES,
+                        ws_bytes - LC_SPLITK_TICKET_BYTES))
+    return LC_OK;
+#endif
   if (tile == 0) {
     // measured on the ViT-B/16 step shapes (tools/bench_gemm.py, M = 50 432): the 256x256
     // phase-interleaved kernel beats the ping-pong one on every shape (776-1113 vs 743-1044 TF)

@@ -335,6 +335,11 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
                   void* out1, long ldo1, const void* aux, long ldaux, const EpiParams& ep,
                   void* ws = nullptr, long ws_bytes = 0);
 
+// hipBLASLt for plain bf16 GEMMs that the step routes there (blaslt.hip, bf16 build only):
+// C[M, N] = A[M, K] . B[N, K]^T, false when hipBLASLt cannot take the launch (nothing written)
+bool lc_blaslt_nt_bf16(hipStream_t stream, int M, int N, int K, const void* A, long lda,
+                       const void* B, long ldb, void* C, long ldo, void* ws, long ws_bytes);
+
 #define LC_CHECK_ARG(cond) \
   do {                     \
     if (!(cond)) return LC_EINVAL; \

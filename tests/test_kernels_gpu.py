@@ -36,6 +36,36 @@ def test_gemm_nt_exact_integers(ops, dev, M, N, K):
     assert torch.equal(out, ref)
 
 
+def test_gemm_qkv_dx_shape_on_hipblaslt(ops, dev):
+    """The one step GEMM routed to hipBLASLt (blaslt.hip): the image tower's QKV input gradient
+    at 256 images (M = 50 432, N = 768, K = 2 304, bf16 out, no bias), through ops.gemm_nt with
+    its split-K workspace: exact on small integers (every partial sum is an integer below 2^24,
+    so any summation order gives the same f32 and bf16-exact result), against torch fp32 on
+    random data, and the same values as gemm8 (a forced tile keeps the hand-written kernel)."""
+    from lcclip import _lib
+    M, N, K = 50432, 768, 2304
+    g = torch.Generator(device=dev).manual_seed(7)
+    A = torch.randint(-2, 3, (M, K), device=dev, generator=g).to(BF)
+    B = torch.randint(-2, 3, (N, K), device=dev, generator=g).to(BF)
+    out = torch.empty(M, N, device=dev, dtype=BF)
+    ops.gemm_nt(A, B, ops.EPI_BF16, out)
+    ref = A.float() @ B.float().t()
+    assert torch.equal(out.float(), ref.to(BF).float())
+    A = (torch.randn(M, K, device=dev, generator=g)).to(BF)
+    B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(BF)
+    ops.gemm_nt(A, B, ops.EPI_BF16, out)
+    ref = A.float() @ B.float().t()
+    assert rel(out, ref) < 4e-3
+    lib = _lib.load()
+    try:
+        assert lib.lc_gemm_set_tile(8) == 0
+        o8 = torch.empty_like(out)
+        ops.gemm_nt(A, B, ops.EPI_BF16, o8)
+    finally:
+        lib.lc_gemm_set_tile(0)
+    assert rel(out, o8) < 4e-3
+
+
 @pytest.mark.parametrize("tile", [1, 2, 3, 5, 7, 8, 11])
 def test_gemm_nt_every_tile_exact(ops, dev, tile):
     """Every tile kernel behind lc_gemm_nt (forced), ragged M, bit-exact on small integers, and
