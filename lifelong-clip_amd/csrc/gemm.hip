@@ -2116,6 +2116,9 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
   }
   int tile = g_force_tile;
 #ifndef LC_F16
+#ifndef LC_BLASLT_MIN_M  // (A/B builds override it)
+#define LC_BLASLT_MIN_M 32768
+#endif
   // the QKV input-gradient GEMM of a 256-image step (plain: no epilogue, no bias) on hipBLASLt
   // (blaslt.hip: 142 vs 160 us standalone, step +1.2 %); its workspace is the split-K scratch
   // after the tickets. A forced tile (A/B tools) or LC_GEMM_BLASLT=0 (DIAG) keeps gemm8.
@@ -2124,7 +2127,7 @@ int lc_gemm_nt_ex(hipStream_t stream, int epi, int M, int N, int K, const void* 
     return !(e && e[0] == '0');
   }();
   if (use_blaslt && tile == 0 && epi == EPI_BF16 && bias == nullptr && alpha == 1.0f &&
-      M >= 32768 && N == 768 && K == 2304 && ws != nullptr &&
+      M >= LC_BLASLT_MIN_M && N == 768 && K == 2304 && ws != nullptr &&
       ws_bytes >= LC_SPLITK_TICKET_BYTES + (8L << 20) &&
       lc_blaslt_nt_bf16(stream, M, N, K, a, lda, b, ldb, out0, ldo0,
                         static_cast<char*>(ws) + LC_SPLITK_TICKET_BYTES,
